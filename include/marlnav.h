@@ -1,0 +1,166 @@
+/*
+ * marlnav.h - C ABI of the MI355X (gfx950) environment-step library
+ * (libmarlnav.so, built from marl-nav_amd/csrc/marlnav_step.hip).
+ *
+ * The reference (JussiM01/MARL-nav) has no FFI: its boundary is the Python
+ * class `Env` (marlnav/environment.py:8-286). Each entry point below replaces
+ * one method of that class; the file:line it replaces is given per function.
+ * The Python host mirror (marl-nav_amd/environment.py) binds these with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every pointer in MarlnavStepBuffers and every array argument is a DEVICE
+ *    pointer (hipMalloc / torch caching allocator), contiguous, fp32 / uint8
+ *    as documented. The library never allocates, frees or synchronises.
+ *  - Every call enqueues its work on `stream` (a hipStream_t; NULL = the
+ *    default stream) and returns immediately.
+ *  - Return value: 0 on success, a negative MARLNAV_E* code otherwise; the
+ *    message is available from marlnav_last_error() (thread-local).
+ *  - Shapes: P = num_parallel, A = num_agents, O = observed obstacles,
+ *    S = obstacle_stride (obstacles stored per env, >= O),
+ *    D = 2 + 2*O + 2*(A-1) observation features per agent.
+ *  - The observation buffer is packed (P, A, D) in the field order of the
+ *    reference's `Observations` namedtuple (utils.py:13-15), which is also the
+ *    concatenation order of `ObsNormalizer` (utils.py:531):
+ *      [target_angle | target_distance | obstacles_angles[O] |
+ *       obstacles_distances[O] | others_angles[A-1] | others_distances[A-1]]
+ */
+#ifndef MARLNAV_H
+#define MARLNAV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MARLNAV_ABI_VERSION 1
+
+/* error codes */
+#define MARLNAV_OK 0
+#define MARLNAV_EINVAL (-1)  /* bad dims / params / null pointer */
+#define MARLNAV_ELAUNCH (-2) /* HIP launch error */
+#define MARLNAV_EUNSUPPORTED (-3)
+
+/* MarlnavParams.flags */
+/* Finished envs take their fresh agent states from the post-move states of
+ * this step instead of fresh_states: reproduces the aliasing of
+ * MockInitializer (utils.py:310-319) on the reference's first step, where
+ * Env.states IS the initializer's tensor and _move_agents mutates it. */
+#define MARLNAV_FRESH_STATES_FROM_MOVED 0x1u
+/* Native re-init draws agent noise (TriangleIntitializer with
+ * noisy_ags=True, utils.py:381-388). The reference ships noisy_ags=False
+ * (utils.py:25). */
+#define MARLNAV_NOISY_AGENTS 0x2u
+/* Also write the ObsNormalizer output (utils.py:519-532) to obs_norm. */
+#define MARLNAV_WRITE_OBS_NORM 0x4u
+/* Apply ActionScaler (utils.py:535-547) to the actions on load: the kernel
+ * reads policy actions in [-1, 1] and scales them itself. */
+#define MARLNAV_SCALE_ACTIONS 0x8u
+
+typedef struct MarlnavDims {
+    int64_t num_parallel;    /* P  (environment.py:15)                        */
+    int32_t num_agents;      /* A  (environment.py:16), 2 <= A <= 64          */
+    int32_t num_obstacles;   /* O  observed per agent (environment.py:17,148) */
+    int32_t obstacle_stride; /* S  = obstacles.shape[1], O <= S <= 256        */
+    int32_t reserved;        /* must be 0                                     */
+    int64_t env_offset;      /* global id of env 0 of this shard (native RNG) */
+} MarlnavDims;
+
+typedef struct MarlnavParams {
+    /* dynamics bounds, environment.py:32-35 */
+    float min_speed, max_speed, min_accel, max_accel;
+    /* truncation: truncated = step_num > trunc_after, with
+     * trunc_after = episode_len - 1 (environment.py:97) */
+    float trunc_after;
+    /* reward weights, environment.py:48-53 */
+    float risk_factor, distance_factor, heading_factor;
+    float target_factor, soft_factor, bond_factor;
+    /* geometric constants, environment.py:56-68 */
+    float ob_risk_dist, ag_risk_dist, ob_coll_dist, ag_coll_dist;
+    float agents_min_d, agents_max_d, max_at_prop_d, max_angle_diff;
+    float target_radius, cap_distance, bond_sharpness, ideal_dist, init_dist;
+    /* native re-init of obstacles, utils.py:344-347, 390-398:
+     * x = obs_range_x * (u - 0.5) + obs_mean_x (same for y) */
+    float obs_range_x, obs_mean_x, obs_range_y, obs_mean_y;
+    /* native noisy agents (MARLNAV_NOISY_AGENTS), utils.py:370-388:
+     * pos += ags_dist * noise_std * N(0,1); heading rotated by
+     * angle_range * (u - 0.5) */
+    float ags_dist, noise_std, angle_range;
+    /* ActionScaler (MARLNAV_SCALE_ACTIONS): a' = scale[k]*a + mean[k] */
+    float act_scale[2], act_mean[2];
+    uint32_t flags;
+    uint32_t reserved;
+    uint64_t seed;           /* native RNG key (Philox4x32-10) */
+} MarlnavParams;
+
+typedef struct MarlnavStepBuffers {
+    /* environment state, updated in place (environment.py:28-30, 38-39) */
+    float *states;           /* (P, A, 5): x, y, dir_x, dir_y, speed       */
+    float *obstacles;        /* (P, S, 2)                                  */
+    float *target;           /* (P, 1, 2)                                  */
+    float *step_num;         /* (P,)                                       */
+    uint8_t *terminates;     /* (P,) bool: reach-target delayed flag       */
+    /* inputs */
+    const float *actions;    /* (P, A, 2): angle, acceleration             */
+    /* reference-RNG re-init candidates (the init sampler's output of this
+     * step, environment.py:78). NULL => native Philox re-init. Only the rows
+     * of finished envs are read. */
+    const float *fresh_states;    /* (P, A, 5) */
+    const float *fresh_obstacles; /* (P, S, 2) */
+    const float *fresh_target;    /* (P, 1, 2) */
+    /* native re-init template: A*5 agent states then 2 target coords */
+    const float *formation;
+    /* outputs */
+    float *obs;              /* (P, A, D) packed Observations              */
+    float *reward;           /* (P,)                                       */
+    uint8_t *terminated;     /* (P,) bool                                  */
+    uint8_t *truncated;      /* (P,) bool                                  */
+    /* episode statistics accumulators: 3 rows (trunc, col, tar) of
+     * marlnav_counter_slots() uint64 partial sums, added to in place */
+    uint64_t *counters;
+    /* optional fused ObsNormalizer (MARLNAV_WRITE_OBS_NORM) */
+    float *obs_norm;         /* (P, A, D)                                  */
+    const float *norm_mean;  /* (D,)                                       */
+    const float *norm_scale; /* (D,)                                       */
+} MarlnavStepBuffers;
+
+/* Env.step(actions) - environment.py:92-107 (with _move_agents :113-137,
+ * observations :139-180, _rews_and_terms :184-269, _reinit :76-90).
+ * step_idx keys the native RNG (any value when fresh_* are given). */
+int marlnav_step(const MarlnavDims *dims, const MarlnavParams *params,
+                 const MarlnavStepBuffers *bufs, uint64_t step_idx,
+                 void *stream);
+
+/* Env.observations() - environment.py:139-180. obs: (P, A, D). */
+int marlnav_observe(const MarlnavDims *dims, const float *states,
+                    const float *obstacles, const float *target, float *obs,
+                    void *stream);
+
+/* Native TriangleIntitializer.__call__ for every env (utils.py:375-398), as
+ * used by Env.__init__ (environment.py:26-30): writes states/obstacles/target
+ * from the formation template and the Philox stream at step_idx. */
+int marlnav_reinit_all(const MarlnavDims *dims, const MarlnavParams *params,
+                       const float *formation, float *states,
+                       float *obstacles, float *target, uint64_t step_idx,
+                       void *stream);
+
+/* Number of uint64 partial-sum slots per counter row for these dims. */
+int64_t marlnav_counter_slots(const MarlnavDims *dims);
+
+/* Sum the counter slots: out3[0..2] = (num_trunc, num_col, num_tar)
+ * (environment.py:43-45, 98, 210-211). out3 is a device pointer. */
+int marlnav_counters_total(const MarlnavDims *dims, const uint64_t *counters,
+                           uint64_t *out3, void *stream);
+
+/* Message of the last failing call on this thread. */
+const char *marlnav_last_error(void);
+
+/* MARLNAV_ABI_VERSION of the built library. */
+int marlnav_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MARLNAV_H */

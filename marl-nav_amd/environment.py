@@ -1,0 +1,475 @@
+"""Drop-in ``Env`` for marlnav/environment.py:8-286 on MI355X.
+
+Same constructor dict, same methods (``step``, ``reset``, ``observations``,
+``sample_actions``), same attributes (``states``, ``obstacles``, ``target``,
+``_step_num``, ``_terminates``, ``_reinit_mask``, the episode counters
+``_num_trunc/_num_col/_num_tar`` and the reward/geometry constants), same
+return types and shapes. The per-step work is one launch of libmarlnav.so
+(include/marlnav.h) on the current HIP stream; nothing on the step path
+synchronises with the host.
+
+Differences from the reference, all deliberate:
+
+* ``states``/``obstacles``/``target`` are device buffers updated in place by
+  each step (the reference rebinds them to new tensors); clone to snapshot.
+* The episode counters live on the device; reading one synchronises.
+* Re-initialisation randomness: ``params['rng']`` selects
+  ``'native'`` (default for the triangle init: a Philox4x32-10 stream keyed
+  by (seed, global env id, step), drawn on the GPU only for finished envs) or
+  ``'reference'`` (the host init sampler is called every step, consuming the
+  torch RNG exactly as the reference does, and finished envs take its rows).
+  A user-assigned ``env._init_sampler`` is always honoured (reference mode).
+"""
+import ctypes
+import math
+
+import torch
+
+from . import abi
+from .utils import MockInitializer, Observations, action_sampler, init_sampler
+
+_F32 = torch.float32
+
+# Env attribute -> MarlnavParams field (environment.py:32-68)
+_PARAM_ATTRS = {
+    'min_speed': 'min_speed', 'max_speed': 'max_speed',
+    'min_accel': 'min_accel', 'max_accel': 'max_accel',
+    '_risk_factor': 'risk_factor', '_distance_factor': 'distance_factor',
+    '_heading_factor': 'heading_factor', '_target_factor': 'target_factor',
+    '_soft_factor': 'soft_factor', '_bond_factor': 'bond_factor',
+    '_ob_risk_dist': 'ob_risk_dist', '_ag_risk_dist': 'ag_risk_dist',
+    '_ob_coll_dist': 'ob_coll_dist', '_ag_coll_dist': 'ag_coll_dist',
+    '_agents_min_d': 'agents_min_d', '_agents_max_d': 'agents_max_d',
+    '_max_at_prop_d': 'max_at_prop_d', '_max_angle_diff': 'max_angle_diff',
+    '_target_radius': 'target_radius', '_cap_distance': 'cap_distance',
+    '_bond_sharpness': 'bond_sharpness', '_ideal_dist': 'ideal_dist',
+    '_init_dist': 'init_dist', 'episode_len': None,
+}
+
+
+def _f32(x):
+    """Python scalar -> the fp32 value torch uses when it meets an fp32 tensor."""
+    return float(torch.tensor(float(x), dtype=_F32))
+
+
+# geometric constants of the reference, environment.py:56-68
+GEOMETRY = {
+    '_ob_risk_dist': 60., '_ag_risk_dist': 15., '_ob_coll_dist': 50.,
+    '_ag_coll_dist': 5., '_agents_min_d': 30., '_agents_max_d': 50.,
+    '_max_at_prop_d': 2, '_max_angle_diff': math.pi / 8, '_target_radius': 30.,
+    '_cap_distance': 0.1, '_bond_sharpness': 1., '_ideal_dist': 40.,
+    '_init_dist': 1200.,
+}
+
+
+def make_cparams(values, init=None, seed=0, flags=0):
+    """Build the kernel's MarlnavParams from Env-attribute-named values
+    (``min_speed``, ``_risk_factor``, ..., ``episode_len``; geometry defaults
+    to GEOMETRY) and, for native re-init, the TriangleIntitializer ``init``.
+    Every value is rounded to fp32 the way torch rounds a Python scalar that
+    meets an fp32 tensor."""
+    v = dict(GEOMETRY)
+    v.update(values)
+    p = abi.MarlnavParams()
+    for attr, field in _PARAM_ATTRS.items():
+        if field is not None:
+            setattr(p, field, _f32(v[attr]))
+    p.trunc_after = _f32(v['episode_len'] - 1)              # environment.py:97
+    keep = flags & ~abi.NOISY_AGENTS
+    if init is not None:
+        p.obs_range_x = _f32(init._obs_x_range)              # utils.py:344-347
+        p.obs_mean_x = _f32(init._obs_mean_x)
+        p.obs_range_y = _f32(init._obs_y_range)
+        p.obs_mean_y = _f32(init._obs_mean_y)
+        p.ags_dist = _f32(init.ags_dist)
+        p.noise_std = _f32(math.sqrt(init.ags_std))
+        p.angle_range = _f32(init.angle_range)
+        if init.noisy_ags:
+            keep |= abi.NOISY_AGENTS
+    p.flags = keep
+    p.seed = int(seed) & (2 ** 64 - 1)
+    return p
+
+
+def _stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Env(object):
+    """Parallel multi-agent navigation environment (environment.py:8)."""
+
+    def __init__(self, params):
+        object.__setattr__(self, '_params_dirty', True)
+        self.params = params
+        self.device = torch.device(params['device'])
+        if self.device.type != 'cuda' or not torch.cuda.is_available():
+            raise RuntimeError(
+                "marlnav_amd.Env runs on a HIP device (params['device'] must be a "
+                f"visible cuda/HIP device, got {params['device']!r}); "
+                "there is no CPU fallback")
+        if self.device.index is None:
+            self.device = torch.device('cuda', torch.cuda.current_device())
+        self._lib = abi.load_library()
+        self.num_parallel = int(params['num_parallel'])
+        self.num_agents = int(params['num_agents'])
+        self.num_obstacles = int(params['num_obstacles'])
+        self.max_step = params['max_step']
+        self.episode_len = params['episode_len']
+        init_p = dict(params['init'])
+        if init_p.get('init_method') == 'triangle':
+            init_p.setdefault('num_agents', self.num_agents)
+        self._init_sampler = init_sampler(init_p)
+        self._default_init_sampler = self._init_sampler
+        self._sampler = action_sampler(params['sampler'])
+        self._others_inds = torch.tensor(
+            [[i for i in range(self.num_agents) if i != j]
+             for j in range(self.num_agents)], device=self.device)
+
+        self.min_speed = params['min_speed']
+        self.max_speed = params['max_speed']
+        self.min_accel = params['min_accel']
+        self.max_accel = params['max_accel']
+        self._risk_factor = params['risk_factor']
+        self._distance_factor = params['distance_factor']
+        self._heading_factor = params['heading_factor']
+        self._target_factor = params['target_factor']
+        self._soft_factor = params['soft_factor']
+        self._bond_factor = params['bond_factor']
+        for name, value in GEOMETRY.items():   # environment.py:56-68
+            setattr(self, name, value)
+
+        rng = params.get('rng', 'native')
+        if rng not in ('native', 'reference'):
+            raise ValueError(f"params['rng'] must be 'native' or 'reference', got {rng!r}")
+        is_triangle = init_p.get('init_method') == 'triangle'
+        self._rng = rng if is_triangle else 'reference'
+        self._mock_alias = init_p.get('init_method') == 'mock_init'
+        self._env_offset = int(params.get('env_offset', 0))
+        seed = params.get('seed', init_p.get('seed'))
+        if seed is None:
+            # native mode only: the reference-RNG path must not touch the torch
+            # generator before the init sampler does (environment.py:26)
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self._rng == 'native' else 0
+        self._seed = int(seed) & (2 ** 64 - 1)
+        self._step_idx = 0
+        self._normalizer = None
+        self._obs_norm_buffers = None
+
+        self._dims = abi.MarlnavDims()
+        self._cparams = abi.MarlnavParams()
+        self._bufs = abi.MarlnavStepBuffers()
+        self._formation = None
+        if is_triangle:
+            smp = self._init_sampler
+            form = torch.cat([smp.formation.reshape(-1), smp.target_point.reshape(-1)])
+            self._formation = form.to(self.device, _F32).contiguous()
+
+        # state buffers
+        P, A = self.num_parallel, self.num_agents
+        if self._rng == 'native':
+            S = self.num_obstacles
+            self._set_state_buffers(torch.empty(P, A, 5, device=self.device),
+                                    torch.empty(P, S, 2, device=self.device),
+                                    torch.empty(P, 1, 2, device=self.device))
+            self._sync_params()
+            abi.check(self._lib.marlnav_reinit_all(
+                ctypes.byref(self._dims), ctypes.byref(self._cparams),
+                self._formation.data_ptr(), self._states.data_ptr(),
+                self._obstacles.data_ptr(), self._target.data_ptr(), 0,
+                _stream_handle(self.device)), self._lib)
+        else:
+            st, ob, tg = self._init_sampler()
+            self._set_state_buffers(st, ob, tg)
+        self._step_idx = 1
+        self._step_num = torch.zeros(P, device=self.device)
+        self._terminates = torch.zeros(P, dtype=torch.bool, device=self.device)
+        self._reinit_mask = torch.zeros(P, device=self.device)
+        self._last_finished = None
+        self._counters = torch.zeros(3, self._slots(), dtype=torch.int64,
+                                     device=self.device)
+        self._counter_out = torch.zeros(3, dtype=torch.int64, device=self.device)
+
+    # ------------------------------------------------------------ plumbing
+    def __setattr__(self, name, value):
+        if name in _PARAM_ATTRS:
+            object.__setattr__(self, '_params_dirty', True)
+        object.__setattr__(self, name, value)
+
+    def _slots(self):
+        n = self._lib.marlnav_counter_slots(ctypes.byref(self._dims))
+        if n < 0:
+            abi.check(-1, self._lib)
+        return n
+
+    def _dev_f32(self, t, shape=None):
+        t = torch.as_tensor(t)
+        t = t.to(device=self.device, dtype=_F32).contiguous()
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise ValueError(f"expected shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t
+
+    def _set_state_buffers(self, states=None, obstacles=None, target=None):
+        """Adopt new state tensors as the env's device buffers. Tensors that
+        could alias caller storage are copied, since steps update in place."""
+        P, A = self.num_parallel, self.num_agents
+
+        def own(value, shape=None):
+            t = self._dev_f32(value, shape)
+            if isinstance(value, torch.Tensor) and t.data_ptr() == value.data_ptr():
+                t = t.clone()
+            return t
+
+        if states is not None:
+            object.__setattr__(self, '_states', own(states, (P, A, 5)))
+        if obstacles is not None:
+            ob = own(obstacles)
+            if ob.dim() != 3 or ob.shape[0] != P or ob.shape[2] != 2:
+                raise ValueError(f"obstacles must be (P, S, 2), got {tuple(ob.shape)}")
+            object.__setattr__(self, '_obstacles', ob)
+        if target is not None:
+            object.__setattr__(self, '_target', own(target, (P, 1, 2)))
+        self._update_dims()
+
+    def _update_dims(self):
+        S = int(self._obstacles.shape[1])
+        d = self._dims
+        old = (d.num_agents, d.num_obstacles, d.obstacle_stride)
+        d.num_parallel = self.num_parallel
+        d.num_agents = self.num_agents
+        d.num_obstacles = min(self.num_obstacles, S)   # environment.py:148-152
+        d.obstacle_stride = S
+        d.reserved = 0
+        d.env_offset = self._env_offset
+        self._obs_dim = 2 + 2 * d.num_obstacles + 2 * (self.num_agents - 1)
+        O = d.num_obstacles
+        self._split = [1, 1, O, O, self.num_agents - 1, self.num_agents - 1]
+        if hasattr(self, '_counters') and old != (d.num_agents, d.num_obstacles, S):
+            totals = self._counter_totals()
+            self._counters = torch.zeros(3, self._slots(), dtype=torch.int64,
+                                         device=self.device)
+            self._counters[:, 0] = torch.tensor(totals, device=self.device)
+
+    def _sync_params(self):
+        if not self._params_dirty:
+            return
+        values = {attr: getattr(self, attr) for attr in _PARAM_ATTRS}
+        init = self._init_sampler if self._formation is not None else None
+        self._cparams = make_cparams(values, init=init, seed=self._seed,
+                                     flags=self._cparams.flags)
+        object.__setattr__(self, '_params_dirty', False)
+
+    def _new_obs(self):
+        return torch.empty(self.num_parallel, self.num_agents, self._obs_dim,
+                           dtype=_F32, device=self.device)
+
+    def _wrap_obs(self, packed, normalized=None):
+        obs = Observations(*torch.split(packed, self._split, dim=2))
+        return _PackedObservations(obs, packed, normalized, self._normalizer)
+
+    # ------------------------------------------------------------ state API
+    @property
+    def states(self):
+        return self._states
+
+    @states.setter
+    def states(self, value):
+        self._set_state_buffers(states=value)
+
+    @property
+    def obstacles(self):
+        return self._obstacles
+
+    @obstacles.setter
+    def obstacles(self, value):
+        self._set_state_buffers(obstacles=value)
+
+    @property
+    def target(self):
+        return self._target
+
+    @target.setter
+    def target(self, value):
+        self._set_state_buffers(target=value)
+
+    @property
+    def _step_num(self):
+        return self.__dict__['_step_num_t']
+
+    @_step_num.setter
+    def _step_num(self, value):
+        self.__dict__['_step_num_t'] = self._dev_f32(value, (self.num_parallel,))
+
+    @property
+    def _terminates(self):
+        return self.__dict__['_terminates_t']
+
+    @_terminates.setter
+    def _terminates(self, value):
+        t = torch.as_tensor(value).to(device=self.device, dtype=torch.bool).contiguous()
+        if tuple(t.shape) != (self.num_parallel,):
+            raise ValueError(f"_terminates must be ({self.num_parallel},)")
+        self.__dict__['_terminates_t'] = t
+
+    @property
+    def _reinit_mask(self):
+        m = self.__dict__.get('_reinit_mask_t')
+        if m is None and self._last_finished is not None:
+            term, trunc = self._last_finished
+            m = torch.where(torch.logical_or(trunc, term), 1, 0)  # environment.py:102-103
+            self.__dict__['_reinit_mask_t'] = m
+        return m
+
+    @_reinit_mask.setter
+    def _reinit_mask(self, value):
+        self.__dict__['_reinit_mask_t'] = value
+
+    # episode statistics (environment.py:43-45); MAPPO reads and zeroes them
+    def _counter_totals(self):
+        abi.check(self._lib.marlnav_counters_total(
+            ctypes.byref(self._dims), self._counters.data_ptr(),
+            self._counter_out.data_ptr(), _stream_handle(self.device)), self._lib)
+        return [int(v) for v in self._counter_out.tolist()]
+
+    def _set_counter(self, row, value):
+        self._counters[row].zero_()
+        self._counters[row, 0] = int(value)
+
+    @property
+    def _num_trunc(self):
+        return self._counter_totals()[0]
+
+    @_num_trunc.setter
+    def _num_trunc(self, v):
+        self._set_counter(0, v)
+
+    @property
+    def _num_col(self):
+        return self._counter_totals()[1]
+
+    @_num_col.setter
+    def _num_col(self, v):
+        self._set_counter(1, v)
+
+    @property
+    def _num_tar(self):
+        return self._counter_totals()[2]
+
+    @_num_tar.setter
+    def _num_tar(self, v):
+        self._set_counter(2, v)
+
+    # ----------------------------------------------------------- public API
+    def attach_normalizer(self, normalizer):
+        """Have every step also write ``normalizer``'s output (utils.py:519-532)
+        from the kernel; ``normalizer(obs)`` then returns it without work."""
+        self._normalizer = normalizer
+        if normalizer is None:
+            self._obs_norm_buffers = None
+            return
+        D = self._obs_dim
+        mean = normalizer.mean.to(self.device, _F32).reshape(-1).contiguous()
+        scale = normalizer.scale.to(self.device, _F32).reshape(-1).contiguous()
+        if mean.numel() != D or scale.numel() != D:
+            raise ValueError(f"normalizer has {mean.numel()} features, env rows have {D}")
+        self._obs_norm_buffers = (mean, scale)
+
+    def reset(self):
+        """environment.py:70-74: marks every env for re-init and returns the
+        current observations (the mask is overwritten by the next step)."""
+        self._reinit_mask = torch.ones(self.num_parallel, device=self.device)
+        return self.observations(), self.params
+
+    def sample_actions(self):
+        """environment.py:109-111"""
+        return self._sampler()
+
+    def observations(self):
+        """environment.py:139-180"""
+        self._sync_params()
+        out = self._new_obs()
+        abi.check(self._lib.marlnav_observe(
+            ctypes.byref(self._dims), self._states.data_ptr(), self._obstacles.data_ptr(),
+            self._target.data_ptr(), out.data_ptr(), _stream_handle(self.device)), self._lib)
+        return self._wrap_obs(out)
+
+    def step(self, actions):
+        """environment.py:92-107: returns (Observations, rewards (P,),
+        terminated (P,) bool, truncated (P,) bool)."""
+        self._sync_params()
+        P, dev = self.num_parallel, self.device
+        if not (isinstance(actions, torch.Tensor) and actions.device == dev
+                and actions.dtype == _F32 and actions.shape[-1] == 2
+                and actions.is_contiguous()):
+            actions = torch.as_tensor(actions)
+            if actions.shape[-1] != 2:
+                actions = actions[..., [0, -1]]  # angle = [..., 0], accel = [..., -1]
+            actions = actions.to(device=dev, dtype=_F32).contiguous()
+        if tuple(actions.shape) != (P, self.num_agents, 2):
+            raise ValueError(f"actions must be ({P}, {self.num_agents}, 2), "
+                             f"got {tuple(actions.shape)}")
+        obs = self._new_obs()
+        reward = torch.empty(P, dtype=_F32, device=dev)
+        terminated = torch.empty(P, dtype=torch.bool, device=dev)
+        truncated = torch.empty(P, dtype=torch.bool, device=dev)
+        b = self._bufs
+        b.states = self._states.data_ptr()
+        b.obstacles = self._obstacles.data_ptr()
+        b.target = self._target.data_ptr()
+        b.step_num = self._step_num.data_ptr()
+        b.terminates = self._terminates.data_ptr()
+        b.actions = actions.data_ptr()
+        b.obs = obs.data_ptr()
+        b.reward = reward.data_ptr()
+        b.terminated = terminated.data_ptr()
+        b.truncated = truncated.data_ptr()
+        b.counters = self._counters.data_ptr()
+        flags = self._cparams.flags & ~(abi.FRESH_STATES_FROM_MOVED | abi.WRITE_OBS_NORM)
+        keep = None
+        if self._rng == 'native' and self._init_sampler is self._default_init_sampler:
+            b.fresh_states = b.fresh_obstacles = b.fresh_target = None
+            b.formation = self._formation.data_ptr()
+        else:
+            fs, fo, ft = self._init_sampler()                # environment.py:78
+            S = self._obstacles.shape[1]
+            keep = (self._dev_f32(fs, (P, self.num_agents, 5)),
+                    self._dev_f32(fo, (P, S, 2)), self._dev_f32(ft, (P, 1, 2)))
+            b.fresh_states, b.fresh_obstacles, b.fresh_target = (t.data_ptr() for t in keep)
+            b.formation = None
+            if self._mock_alias:
+                flags |= abi.FRESH_STATES_FROM_MOVED
+        normalized = None
+        if self._obs_norm_buffers is not None:
+            normalized = self._new_obs()
+            b.obs_norm = normalized.data_ptr()
+            b.norm_mean = self._obs_norm_buffers[0].data_ptr()
+            b.norm_scale = self._obs_norm_buffers[1].data_ptr()
+            flags |= abi.WRITE_OBS_NORM
+        self._cparams.flags = flags
+        abi.check(self._lib.marlnav_step(
+            ctypes.byref(self._dims), ctypes.byref(self._cparams), ctypes.byref(b),
+            self._step_idx, _stream_handle(dev)), self._lib)
+        self._step_idx += 1
+        if self._mock_alias:
+            # the reference's MockInitializer now holds the post-move states
+            # (utils.py:310-319 aliasing); later re-inits restore them
+            self._mock_alias = False
+            init = self._init_sampler
+            if isinstance(init, MockInitializer):
+                init.states = self._states.clone()
+        self._last_finished = (terminated, truncated)
+        self.__dict__['_reinit_mask_t'] = None
+        del keep
+        return self._wrap_obs(obs, normalized), reward, terminated, truncated
+
+
+class _PackedObservations(Observations):
+    """``Observations`` whose six fields are views of one packed (P, A, D)
+    tensor (the layout of ObsNormalizer's torch.cat, utils.py:531); carries
+    that tensor and, when a normalizer is attached, the kernel-normalized one."""
+
+    def __new__(cls, obs, packed, normalized, normalizer):
+        self = super().__new__(cls, *obs)
+        self._packed = packed
+        self._normalized = normalized
+        self._normalizer = normalizer
+        return self

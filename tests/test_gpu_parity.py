@@ -1,0 +1,284 @@
+"""Parity of the HIP step (libmarlnav.so through the drop-in Env) with the
+reference's golden vectors and with the C oracle. Needs an MI355X."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import (OBS_FIELDS, assert_obs_close, assert_states_close, assert_vec_close,
+                      cli_args, env_values, golden, meta)
+
+import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+STEP_CASES = ["step_a3o3", "step_a3o8", "step_a16o32", "step_a2o1", "step_p1"]
+DEV = "cuda"
+
+
+def np_(t):
+    return t.detach().cpu().numpy()
+
+
+def make_env(pkg, P, A, O, episode_len=200, rng="native", seed=1234, factors=None,
+             sampler_num=-1, env_offset=0, **init_over):
+    args = cli_args(num_parallel=P, num_agents=A, num_obstacles=O, episode_len=episode_len,
+                    sampler_num=sampler_num, max_step=1000, **(factors or {}))
+    params = pkg.set_env_params(args, DEV)
+    params["init"] = dict(params["init"], **init_over)
+    if params["sampler"] is not None:
+        params["sampler"] = dict(params["sampler"])
+    params["rng"] = rng
+    params["seed"] = seed
+    params["env_offset"] = env_offset
+    return pkg.Env(params)
+
+
+def fields_np(obs):
+    return [np_(getattr(obs, f)) for f in OBS_FIELDS]
+
+
+def oracle_params(env):
+    env._sync_params()
+    return env._dims, env._cparams
+
+
+@pytest.mark.parametrize("name", STEP_CASES)
+def test_step_matches_reference_golden(pkg, name):
+    """F1 through the drop-in API, injecting state exactly as the golden
+    generator injected it into the reference's Env."""
+    m, z = meta(name), golden(name)
+    P, A, O = m["num_parallel"], m["num_agents"], m["num_obstacles"]
+    factors = {k: m[k] for k in ("risk_factor", "distance_factor", "heading_factor",
+                                 "target_factor", "soft_factor", "bond_factor")}
+    env = make_env(pkg, P, A, O, episode_len=m["episode_len"], rng="reference",
+                   factors=factors, noise_device="cpu")
+    for k in range(m["steps"]):
+        env.states = torch.from_numpy(z["in_states"][k])
+        env.obstacles = torch.from_numpy(z["in_obstacles"][k])
+        env.target = torch.from_numpy(z["in_target"][k])
+        env._step_num = torch.from_numpy(z["in_step_num"][k])
+        env._terminates = torch.from_numpy(z["in_terminates"][k])
+        fs, fo, ft = (torch.from_numpy(z[x][k]) for x in
+                      ("fresh_states", "fresh_obstacles", "fresh_target"))
+        env._init_sampler = lambda fs=fs, fo=fo, ft=ft: (fs, fo, ft)
+        obs0 = env.observations()
+        c0 = (env._num_trunc, env._num_col, env._num_tar)
+        obs, rew, term, trunc = env.step(torch.from_numpy(z["actions"][k]).to(DEV))
+        c1 = (env._num_trunc, env._num_col, env._num_tar)
+        where = f"{name} step {k}"
+        np.testing.assert_array_equal(np_(term), z["terminated"][k], where)
+        np.testing.assert_array_equal(np_(trunc), z["truncated"][k], where)
+        np.testing.assert_array_equal(np_(env._terminates), z["out_terminates"][k], where)
+        np.testing.assert_array_equal(np_(env._step_num), z["out_step_num"][k], where)
+        np.testing.assert_array_equal(np_(env.obstacles), z["out_obstacles"][k], where)
+        np.testing.assert_array_equal(np_(env.target), z["out_target"][k], where)
+        assert [b - a for a, b in zip(c0, c1)] == [z["d_trunc"][k], z["d_col"][k],
+                                                     z["d_tar"][k]], where
+        assert_vec_close(np_(rew), z["reward"][k], what=where + " reward")
+        assert_states_close(np_(env.states), z["out_states"][k], where)
+        assert_obs_close(fields_np(obs), {f: z["obs_" + f][k] for f in OBS_FIELDS},
+                         prefix="", where=where)
+        f0 = fields_np(obs0)
+        for f, a in zip(OBS_FIELDS, f0):
+            if "distance" in f:  # correctly rounded sqrt: bit-exact
+                np.testing.assert_array_equal(a, z["obs0_" + f][k], where + " " + f)
+        assert_obs_close(f0, {f: z["obs0_" + f][k] for f in OBS_FIELDS}, prefix="",
+                         where=where + " observe")
+
+
+@pytest.mark.parametrize("name", STEP_CASES)
+def test_step_bit_exact_vs_oracle(pkg, name):
+    """Same injected inputs through the oracle: dynamics, distances, flags
+    and rewards bit for bit; angles within the acosf ulp budget."""
+    m, z = meta(name), golden(name)
+    P, A, O = m["num_parallel"], m["num_agents"], m["num_obstacles"]
+    factors = {k: m[k] for k in ("risk_factor", "distance_factor", "heading_factor",
+                                 "target_factor", "soft_factor", "bond_factor")}
+    env = make_env(pkg, P, A, O, episode_len=m["episode_len"], rng="reference",
+                   factors=factors, noise_device="cpu")
+    dm, pr = oracle_params(env)
+    for k in range(m["steps"]):
+        ins = [z[x][k] for x in ("in_states", "in_obstacles", "in_target", "in_step_num",
+                                 "in_terminates", "actions")]
+        fresh = tuple(z[x][k] for x in ("fresh_states", "fresh_obstacles", "fresh_target"))
+        exp = orc.step(dm, pr, *ins, fresh=fresh)
+        env.states, env.obstacles, env.target = (torch.from_numpy(x) for x in ins[:3])
+        env._step_num = torch.from_numpy(ins[3])
+        env._terminates = torch.from_numpy(ins[4])
+        env._init_sampler = lambda fs=fresh: tuple(torch.from_numpy(x) for x in fs)
+        obs, rew, term, trunc = env.step(torch.from_numpy(ins[5]).to(DEV))
+        where = f"{name} step {k}"
+        np.testing.assert_array_equal(np_(env.states), exp["states"], where)
+        np.testing.assert_array_equal(np_(rew), exp["reward"], where)
+        np.testing.assert_array_equal(np_(term), exp["terminated"], where)
+        np.testing.assert_array_equal(np_(trunc), exp["truncated"], where)
+        got = np_(obs._packed)
+        fo = orc.split_obs(exp["obs"], A, O)
+        fg = orc.split_obs(got, A, O)
+        for f, a, e in zip(OBS_FIELDS, fg, fo):
+            if "distance" in f:
+                np.testing.assert_array_equal(a, e, where + " " + f)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, where=where)
+
+
+def _trace_env(pkg, name):
+    m = meta(name)
+    args = cli_args(sampler_num=m["sampler_num"], max_step=m["steps"])
+    if m["seed"] is not None:
+        pkg.set_all_seeds(m["seed"])
+    params = pkg.set_env_params(args, DEV)
+    params["init"] = dict(params["init"], noise_device="cpu")
+    params["rng"] = "reference"
+    return m, pkg.Env(params)
+
+
+@pytest.mark.parametrize("name", ["trace_cfg1", "trace_mock0", "trace_mock1"])
+def test_trace_matches_reference(pkg, name):
+    """F2/F3: the reward-check loop (utils.py:595-613) for 1000 steps through
+    the drop-in Env, reference RNG mode: identical episodes and counters."""
+    m, env = _trace_env(pkg, name)
+    z = golden(name)
+    np.testing.assert_array_equal(np_(env.states), z["states0"])
+    np.testing.assert_array_equal(np_(env.obstacles), z["obstacles0"])
+    A = env.num_agents
+    O = env._dims.num_obstacles
+    for k in range(m["steps"]):
+        obs, rew, term, trunc = env.step(env.sample_actions())
+        where = f"{name} step {k + 1}"
+        np.testing.assert_array_equal(np_(term), z["terminated"][k], where)
+        np.testing.assert_array_equal(np_(trunc), z["truncated"][k], where)
+        np.testing.assert_array_equal(np_(env.obstacles), z["obstacles"][k], where)
+        assert_states_close(np_(env.states), z["states"][k], where)
+        assert_vec_close(np_(rew), z["reward"][k], what=where + " reward")
+        assert_obs_close(fields_np(obs), {f: z["obs_" + f][k] for f in OBS_FIELDS},
+                         prefix="", where=where)
+        if k % 100 == 99:
+            assert (env._num_trunc, env._num_col, env._num_tar) == (
+                z["num_trunc"][k], z["num_col"][k], z["num_tar"][k]), where
+    assert (env._num_trunc, env._num_col, env._num_tar) == (
+        z["num_trunc"][-1], z["num_col"][-1], z["num_tar"][-1])
+    with pytest.raises(StopIteration) if m["sampler_num"] >= 0 else _nullctx():
+        env.sample_actions()
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+@pytest.mark.parametrize("P,A,O,steps", [(4096, 3, 3, 60), (1000, 3, 8, 40),
+                                         (512, 16, 32, 12), (333, 5, 2, 30),
+                                         (65536, 3, 3, 6)])
+def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps):
+    """Native (Philox) re-init mode, many steps, random actions, short
+    episodes: the GPU trajectory equals the oracle's bit for bit."""
+    g = torch.Generator().manual_seed(P + A + O)
+    env = make_env(pkg, P, A, O, episode_len=25, seed=99,
+                   factors=dict(risk_factor=3., distance_factor=7.))
+    dm, pr = oracle_params(env)
+    form = np_(env._formation)
+    st, ob, tg = orc.reinit_all(dm, pr, form, 0)
+    np.testing.assert_array_equal(np_(env.states), st)
+    np.testing.assert_array_equal(np_(env.obstacles), ob)
+    np.testing.assert_array_equal(np_(env.target), tg)
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    tot = np.zeros(3, np.int64)
+    for k in range(steps):
+        th = (torch.rand(P, A, generator=g) - 0.5) * 0.8
+        acc = (torch.rand(P, A, generator=g) - 0.5) * 1.2
+        acts = torch.stack([th, acc], 2)
+        exp = orc.step(dm, pr, st, ob, tg, sn, te, acts.numpy(), formation=form,
+                       step_idx=k + 1)
+        obs, rew, term, trunc = env.step(acts.to(DEV))
+        where = f"P{P} A{A} O{O} step {k + 1}"
+        np.testing.assert_array_equal(np_(env.states), exp["states"], where)
+        np.testing.assert_array_equal(np_(env.obstacles), exp["obstacles"], where)
+        np.testing.assert_array_equal(np_(env.target), exp["target"], where)
+        np.testing.assert_array_equal(np_(env._step_num), exp["step_num"], where)
+        np.testing.assert_array_equal(np_(env._terminates), exp["terminates"], where)
+        np.testing.assert_array_equal(np_(term), exp["terminated"], where)
+        np.testing.assert_array_equal(np_(trunc), exp["truncated"], where)
+        np.testing.assert_array_equal(np_(rew), exp["reward"], where)
+        got = np_(obs._packed)
+        Oe = dm.num_obstacles
+        fg, fo = orc.split_obs(got, A, Oe), orc.split_obs(exp["obs"], A, Oe)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, where=where)
+        st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
+                                               "terminates"))
+        tot += exp["counters"]
+    assert [env._num_trunc, env._num_col, env._num_tar] == tot.tolist()
+    assert tot[0] > 0 and tot[1] > 0  # both terminal paths exercised
+
+
+def test_counters_reset_like_mappo(pkg):
+    """MAPPO reads then assigns 0 to the counters (models.py:151-158)."""
+    env = make_env(pkg, 2048, 3, 3, episode_len=5)
+    for _ in range(12):
+        env.step(torch.zeros(2048, 3, 2, device=DEV))
+    assert env._num_trunc >= 2048
+    env._num_trunc = 0
+    env._num_col = 0
+    env._num_tar = 7
+    assert (env._num_trunc, env._num_col, env._num_tar) == (0, 0, 7)
+    env.step(torch.zeros(2048, 3, 2, device=DEV))
+    assert env._num_trunc == 0 and env._num_tar == 7
+
+
+def test_fused_normalizer_and_action_scaler(pkg):
+    """§8(f) rows 1-2: ObsNormalizer fused into the step equals the host
+    normalizer (utils.py:519-532) on the returned obs; ActionScaler
+    (utils.py:535-547) applied outside gives the same step."""
+    args = cli_args(num_parallel=3000, num_obstacles=3)
+    nrm = pkg.ObsNormalizer(pkg.set_normalizer_params(args, DEV))
+    scl = pkg.ActionScaler(pkg.set_scaler_params(args, DEV))
+    env = make_env(pkg, 3000, 3, 3, episode_len=15)
+    env.attach_normalizer(nrm)
+    g = torch.Generator().manual_seed(5)
+    for _ in range(20):
+        raw = (torch.rand(3000, 3, 2, generator=g) * 2 - 1).to(DEV)
+        obs, rew, term, trunc = env.step(scl(raw))
+        fused = nrm(obs)
+        ref = (torch.cat(tuple(obs), dim=2) - nrm.mean) / nrm.scale_tensor
+        assert fused is obs._normalized
+        torch.testing.assert_close(fused, ref, rtol=0, atol=0)
+
+
+def test_observations_reset_and_api(pkg):
+    env = make_env(pkg, 10, 3, 3)
+    obs, params = env.reset()
+    assert params is env.params
+    assert isinstance(obs, pkg.Observations)
+    assert [tuple(x.shape) for x in obs] == [(10, 3, 1), (10, 3, 1), (10, 3, 3), (10, 3, 3),
+                                            (10, 3, 2), (10, 3, 2)]
+    assert torch.equal(env._reinit_mask, torch.ones(10, device=DEV))
+    o2, r, te, tr = env.step(env.sample_actions())
+    assert r.shape == (10,) and r.dtype == torch.float32
+    assert te.dtype == torch.bool and tr.dtype == torch.bool
+    assert env._reinit_mask.dtype == torch.int64
+    # non-contiguous / wider actions are accepted like the reference's slicing
+    wide = torch.zeros(10, 3, 4, device=DEV)
+    env.step(wide)
+    with pytest.raises(ValueError):
+        env.step(torch.zeros(9, 3, 2, device=DEV))
+
+
+def test_sharded_native_init_is_invariant(pkg):
+    """Philox keyed on the global env id: two shards == one whole batch."""
+    full = make_env(pkg, 1000, 3, 3, seed=7)
+    a = make_env(pkg, 400, 3, 3, seed=7, env_offset=0)
+    b = make_env(pkg, 600, 3, 3, seed=7, env_offset=400)
+    torch.testing.assert_close(full.obstacles, torch.cat([a.obstacles, b.obstacles]),
+                               rtol=0, atol=0)
+    acts = torch.zeros(1000, 3, 2, device=DEV)
+    acts[:, :, 1] = 0.5
+    for _ in range(30):
+        full.step(acts)
+        a.step(acts[:400])
+        b.step(acts[400:])
+    torch.testing.assert_close(full.states, torch.cat([a.states, b.states]), rtol=0, atol=0)
+    torch.testing.assert_close(full.obstacles, torch.cat([a.obstacles, b.obstacles]),
+                               rtol=0, atol=0)
