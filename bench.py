@@ -66,7 +66,7 @@ def make_env(pkg, P, A, O, device, rank):
     params = pkg.set_env_params(args, device)
     params["rng"] = "native"
     params["seed"] = 20251003
-    params["env_offset"] = rank * P
+    params["env_offset"], _ = pkg.shard.weak_slice(rank, P)
     return pkg.Env(params)
 
 
@@ -168,10 +168,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = pkg.shard.max_over_ranks(dt, device)
 
     kern_avg, kern_med = kernel_time_us(env, actions, a.kernel_steps)
     per_env = alg_bytes_per_env(A, O)
@@ -191,7 +188,7 @@ def main():
                           f"in {secs:.1f} s after 1 warm-up step; host os.cpu_count()="
                           f"{os.cpu_count()}")}
 
-    counters = [env._num_trunc, env._num_col, env._num_tar]
+    counters = pkg.shard.sum_over_ranks([env._num_trunc, env._num_col, env._num_tar], device)
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node) at 3 agents; 1/2/4/8-GPU scaling + %HBM roofline",
@@ -218,7 +215,7 @@ def main():
                          "alg_bytes_per_launch": launch_bytes,
                          "alg_bytes_per_env_step": per_env},
             "cpu_baseline": cpu,
-            "episode_counters_rank0": counters,
+            "episode_counters": counters,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -5,6 +5,6 @@ import importlib as _importlib
 import sys as _sys
 
 _pkg = _importlib.import_module("marl-nav_amd")
-for _name in ("abi", "environment", "utils"):
+for _name in ("abi", "environment", "shard", "utils"):
     _sys.modules[__name__ + "." + _name] = _sys.modules["marl-nav_amd." + _name]
 _sys.modules[__name__] = _pkg
