@@ -32,6 +32,13 @@
 namespace {
 
 constexpr float kPiF = 3.14159265358979323846f;
+
+// Timing-only ablation builds (scripts/kbench.py; never shipped, results
+// wrong by construction): 1 no acos, 2 fast fp32 sin/cos, 4 fast division,
+// 8 fast sqrt, 16 no observation math at all.
+#ifndef MARLNAV_ABLATE
+#define MARLNAV_ABLATE 0
+#endif
 constexpr int kMaxAgents = 64;
 constexpr int kMaxStride = 256;
 constexpr int kLdsBudget = 48 * 1024;
@@ -61,7 +68,11 @@ __device__ __forceinline__ float clamp_t(float x, float lo, float hi)
 __device__ __forceinline__ float pair_dist(float ox, float oy, float px, float py)
 {
     const float dx = px - ox, dy = py - oy;
+#if MARLNAV_ABLATE & 8
+    return __builtin_amdgcn_sqrtf(__builtin_fmaf(dy, dy, dx * dx));
+#else
     return __builtin_sqrtf(__builtin_fmaf(dy, dy, dx * dx));
+#endif
 }
 
 // _get_angles (environment.py:276-286) + the dist < 0.1 cap (:172-177)
@@ -70,20 +81,32 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
 {
     const float dx = px - ox, dy = py - oy;
     const float den = dist > 1e-12f ? dist : 1e-12f;
+#if MARLNAV_ABLATE & 4
+    const float nx = __fdividef(dx, den), ny = __fdividef(dy, den);
+#else
     const float nx = dx / den, ny = dy / den;
+#endif
     float dot = dirx * nx + diry * ny;
     dot = clamp_t(dot, -1.0f, 1.0f);
     const float orth_x = nx - dot * dirx;
+#if MARLNAV_ABLATE & 1
+    const float ang = (orth_x > 0.0f ? -1.0f : 1.0f) * dot;
+#else
     const float ang = (orth_x > 0.0f ? -1.0f : 1.0f) * acosf(dot);
+#endif
     return dist < cap ? 0.0f : ang;
 }
 
 __device__ __forceinline__ void sincos_rn(float th, float *s, float *c)
 {
+#if MARLNAV_ABLATE & 2
+    __sincosf(th, s, c);
+#else
     double sd, cd;
     sincos((double)th, &sd, &cd);
     *s = (float)sd;
     *c = (float)cd;
+#endif
 }
 
 // ----------------------------------------------------------- native RNG
@@ -178,6 +201,75 @@ __device__ __forceinline__ void tile_store(float *__restrict__ dst, const float 
         head = n4 << 2;
     }
     for (int i = head + tid; i < n; i += nthr) dst[i] = src[i];
+}
+
+// Stage three contiguous global ranges into LDS with every global load of
+// the tile issued before the first wait: up to KMAX 16-byte vectors per
+// lane are held in registers, then written to LDS. (A load -> LDS-store ->
+// next-load loop would pay one full memory round trip per iteration.)
+struct Span {
+    const float *src;
+    float *dst;
+    int n;  // floats
+};
+
+template <int KMAX>
+__device__ __forceinline__ void stage_spans(Span a, Span b, Span c, int tid, int nthr)
+{
+    const bool vec = ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(b.src) |
+                       reinterpret_cast<uintptr_t>(c.src)) & 15u) == 0 && nthr >= 12;
+    if (!vec) {  // unaligned shard base: plain scalar staging
+        tile_load(a.dst, a.src, a.n, tid, nthr);
+        tile_load(b.dst, b.src, b.n, tid, nthr);
+        tile_load(c.dst, c.src, c.n, tid, nthr);
+        return;
+    }
+    const int va = a.n >> 2, vb = b.n >> 2, vc = c.n >> 2;
+    const int vt = va + vb + vc;
+    float4 r[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int i = tid + k * nthr;
+        if (i < vt) {
+            const float *p = i < va ? a.src + 4 * i
+                                    : (i < va + vb ? b.src + 4 * (i - va) : c.src + 4 * (i - va - vb));
+            r[k] = *reinterpret_cast<const float4 *>(p);
+        }
+    }
+    // scalar tails (< 4 floats per span), one lane per float
+    float t = 0.0f;
+    const int ta = a.n & 3, tb = b.n & 3, tc = c.n & 3;
+    const int lane_t = tid - (nthr - 12);  // last 12 lanes take the tails
+    const float *tsrc = nullptr;
+    float *tdst = nullptr;
+    if (lane_t >= 0) {
+        const int j = lane_t & 3, w = lane_t >> 2;
+        const Span &sp = w == 0 ? a : (w == 1 ? b : c);
+        const int tn = w == 0 ? ta : (w == 1 ? tb : tc);
+        if (j < tn) {
+            tsrc = sp.src + (sp.n & ~3) + j;
+            tdst = sp.dst + (sp.n & ~3) + j;
+            t = *tsrc;
+        }
+    }
+    // generic tiles with more vectors than KMAX per lane
+    for (int i = tid + KMAX * nthr; i < vt; i += nthr) {
+        const float *p = i < va ? a.src + 4 * i
+                                : (i < va + vb ? b.src + 4 * (i - va) : c.src + 4 * (i - va - vb));
+        float *q = i < va ? a.dst + 4 * i
+                          : (i < va + vb ? b.dst + 4 * (i - va) : c.dst + 4 * (i - va - vb));
+        *reinterpret_cast<float4 *>(q) = *reinterpret_cast<const float4 *>(p);
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int i = tid + k * nthr;
+        if (i < vt) {
+            float *q = i < va ? a.dst + 4 * i
+                              : (i < va + vb ? b.dst + 4 * (i - va) : c.dst + 4 * (i - va - vb));
+            *reinterpret_cast<float4 *>(q) = r[k];
+        }
+    }
+    if (tdst) *tdst = t;
 }
 
 // ObsNormalizer fused into the store (utils.py:530-532)
@@ -402,10 +494,18 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
     const MarlnavStepBuffers &b = args.b;
     const bool norm = (pr.flags & MARLNAV_WRITE_OBS_NORM) != 0;
 
-    // ---- phase 0: stage the tile
-    tile_load(st, b.states + e0 * A * 5, nr * 5, tid, nthr);
-    tile_load(ob, b.obstacles + e0 * S * 2, ne * S * 2, tid, nthr);
-    tile_load(tg, b.target + e0 * 2, ne * 2, tid, nthr);
+    // ---- phase 0: stage the tile (all global loads in flight together)
+    float2 act = make_float2(0.0f, 0.0f);
+    if (tid < nr) act = reinterpret_cast<const float2 *>(b.actions)[e0 * A + tid];
+    float step_num_in = 0.0f;
+    uint8_t term_in = 0;
+    if (tid < ne) {
+        step_num_in = b.step_num[e0 + tid];
+        term_in = b.terminates[e0 + tid];
+    }
+    stage_spans<4>(Span{b.states + e0 * A * 5, st, nr * 5},
+                   Span{b.obstacles + e0 * S * 2, ob, ne * S * 2},
+                   Span{b.target + e0 * 2, tg, ne * 2}, tid, nthr);
     if (norm) {
         for (int k = tid; k < D; k += nthr) {
             lds[tp.off_nm + k] = b.norm_mean[k];
@@ -413,8 +513,6 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
         }
     }
     if (tid < 3) cnt[tid] = 0u;
-    float2 act = make_float2(0.0f, 0.0f);
-    if (tid < nr) act = reinterpret_cast<const float2 *>(b.actions)[e0 * A + tid];
     __syncthreads();
 
     // ---- phase 1: _move_agents (environment.py:113-123)
@@ -442,7 +540,7 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
     __syncthreads();
 
     // ---- phase 2: observations of the moved state + reward terms (:99-100)
-    if (tid < nr) {
+    if (tid < nr && !(MARLNAV_ABLATE & 16)) {
         const RowOut ro = observe_row<A_T, O_T, true>(A, O, st + 5 * A * el, ob + 2 * S * el,
                                                       tg + 2 * el, a, obs + tid * D, pr);
         rmiss[tid] = ro.r_miss;
@@ -464,9 +562,9 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
         const float rsum = torch_row_sum(rr + tid * A, A, [](float r) { return r; });
         b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
 
-        float step_num = b.step_num[e] + 1.0f;             // :96
+        float step_num = step_num_in + 1.0f;               // :96
         const bool truncated = step_num > pr.trunc_after;  // :97
-        const bool term_old = b.terminates[e] != 0;
+        const bool term_old = term_in != 0;
         const bool terminated = any_col || term_old;       // :213-214
         b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
         b.terminated[e] = (uint8_t)terminated;
@@ -538,9 +636,9 @@ __global__ void __launch_bounds__(1024) observe_kernel(StepArgs args)
     float *ob = lds + tp.off_ob;
     float *tg = lds + tp.off_tg;
     float *obs = lds + tp.off_obs;
-    tile_load(st, args.b.states + e0 * A * 5, nr * 5, tid, nthr);
-    tile_load(ob, args.b.obstacles + e0 * S * 2, ne * S * 2, tid, nthr);
-    tile_load(tg, args.b.target + e0 * 2, ne * 2, tid, nthr);
+    stage_spans<4>(Span{args.b.states + e0 * A * 5, st, nr * 5},
+                   Span{args.b.obstacles + e0 * S * 2, ob, ne * S * 2},
+                   Span{args.b.target + e0 * 2, tg, ne * 2}, tid, nthr);
     __syncthreads();
     if (tid < nr) {
         const int el = tid / A, a = tid - el * A;

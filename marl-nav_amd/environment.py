@@ -253,7 +253,7 @@ class Env(object):
         if not self._params_dirty:
             return
         values = {attr: getattr(self, attr) for attr in _PARAM_ATTRS}
-        init = self._init_sampler if self._formation is not None else None
+        init = self._default_init_sampler if self._formation is not None else None
         self._cparams = make_cparams(values, init=init, seed=self._seed,
                                      flags=self._cparams.flags)
         object.__setattr__(self, '_params_dirty', False)
