@@ -39,6 +39,28 @@ constexpr float kPiF = 3.14159265358979323846f;
 #ifndef MARLNAV_ABLATE
 #define MARLNAV_ABLATE 0
 #endif
+
+// Diagnostic build (MARLNAV_STAMPS=1, scripts/kstamps.py): lane 0 of every
+// block records s_memrealtime / s_memtime at each phase boundary into a
+// buffer registered with marlnav_debug_stamps(). Never in the shipped build.
+#ifndef MARLNAV_STAMPS
+#define MARLNAV_STAMPS 0
+#endif
+#if MARLNAV_STAMPS
+__device__ unsigned long long *g_stamps;
+#define STAMP(k)                                                                   \
+    do {                                                                           \
+        if (threadIdx.x == 0) {                                                    \
+            unsigned long long *sp_ = g_stamps + (size_t)blockIdx.x * 16;          \
+            sp_[2 * (k)] = wall_clock64();                                         \
+            sp_[2 * (k) + 1] = clock64();                                          \
+        }                                                                          \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
 constexpr int kMaxAgents = 64;
 constexpr int kMaxStride = 256;
 constexpr int kLdsBudget = 48 * 1024;
@@ -494,6 +516,7 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
     const MarlnavStepBuffers &b = args.b;
     const bool norm = (pr.flags & MARLNAV_WRITE_OBS_NORM) != 0;
 
+    STAMP(0);
     // ---- phase 0: stage the tile (all global loads in flight together)
     float2 act = make_float2(0.0f, 0.0f);
     if (tid < nr) act = reinterpret_cast<const float2 *>(b.actions)[e0 * A + tid];
@@ -514,6 +537,7 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
     }
     if (tid < 3) cnt[tid] = 0u;
     __syncthreads();
+    STAMP(1);
 
     // ---- phase 1: _move_agents (environment.py:113-123)
     const int el = tid / A, a = tid - el * A;
@@ -538,6 +562,7 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
         s[4] = v;
     }
     __syncthreads();
+    STAMP(2);
 
     // ---- phase 2: observations of the moved state + reward terms (:99-100)
     if (tid < nr && !(MARLNAV_ABLATE & 16)) {
@@ -548,6 +573,7 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
         rfl[tid] = ro.flags;
     }
     __syncthreads();
+    STAMP(3);
 
     // ---- phase 3: per-env reductions, terminal logic, masked re-init
     if (tid < ne) {
@@ -598,6 +624,7 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
         envbits[tid] = bits;
     }
     __syncthreads();
+    STAMP(4);
 
     // ---- phase 4: observations of re-initialised envs (:105)
     if (tid < nr && (envbits[el] & kFin)) {
@@ -605,6 +632,7 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
                                      obs + tid * D, pr);
     }
     __syncthreads();
+    STAMP(5);
 
     // ---- phase 5: stream the tile out
     tile_store(b.states + e0 * A * 5, st, nr * 5, tid, nthr);
@@ -616,6 +644,11 @@ __global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams
         const unsigned v = cnt[tid];
         if (v) b.counters[tid * args.slots + blockIdx.x] += v;
     }
+    STAMP(6);
+#if MARLNAV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(7);
+#endif
 }
 
 // ------------------------------------------------------------ observe kernel
@@ -750,6 +783,14 @@ StepArgs make_args(const MarlnavDims *d, int E)
 extern "C" {
 
 int marlnav_abi_version(void) { return MARLNAV_ABI_VERSION; }
+
+#if MARLNAV_STAMPS
+int marlnav_debug_stamps(void *buf)
+{
+    const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf));
+    return e == hipSuccess ? 0 : fail(MARLNAV_ELAUNCH, "stamps: %s", hipGetErrorString(e));
+}
+#endif
 
 const char *marlnav_last_error(void) { return g_err; }
 

@@ -1,0 +1,61 @@
+"""Per-phase timeline of the step kernel from the MARLNAV_STAMPS build
+(marl-nav_amd/lib/stamps.so): block dispatch spread and phase durations."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["MARLNAV_LIB"] = os.path.join(ROOT, "marl-nav_amd", "lib", "stamps.so")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    import marlnav_amd as pkg
+    cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["65536x3x3"]
+    names = ["staged", "moved", "observed", "env", "reobs", "stored", "drained"]
+    for cfg in cfgs:
+        P, A, O = (int(x) for x in cfg.split("x"))
+        params = pkg.set_env_params(pkg.default_args(num_parallel=P, num_agents=A,
+                                                     num_obstacles=O), "cuda")
+        params["rng"], params["seed"] = "native", 5
+        env = pkg.Env(params)
+        lib = env._lib
+        lib.marlnav_debug_stamps.argtypes = [ctypes.c_void_p]
+        nb = env._counters.shape[1]
+        buf = torch.zeros(nb * 16, dtype=torch.int64, device="cuda")
+        assert lib.marlnav_debug_stamps(buf.data_ptr()) == 0
+        acts = torch.zeros(P, A, 2, device="cuda")
+        acts[..., 0] = 0.1
+        for _ in range(5):
+            env.step(acts)
+        torch.cuda.synchronize()
+        res = []
+        for _ in range(5):
+            env.step(acts)
+            torch.cuda.synchronize()
+            st = buf.view(nb, 8, 2).cpu().numpy().astype(np.int64)
+            rt = st[:, :, 0] * 10.0 / 1e3  # 100 MHz ticks -> us
+            cy = st[:, :, 1]
+            t0 = rt[:, 0].min()
+            ph = np.diff(rt, axis=1)
+            clk = (cy[:, 7] - cy[:, 0]) / np.maximum(rt[:, 7] - rt[:, 0], 1e-3) / 1e3
+            res.append({
+                "span_us": round(float(rt[:, 7].max() - t0), 2),
+                "start_spread_us": round(float(rt[:, 0].max() - t0), 2),
+                "last_stored_us": round(float(rt[:, 6].max() - t0), 2),
+                "phase_median_us": {n: round(float(np.median(ph[:, i])), 3)
+                                    for i, n in enumerate(names)},
+                "phase_p90_us": {n: round(float(np.percentile(ph[:, i], 90)), 3)
+                                 for i, n in enumerate(names)},
+                "block_total_median_us": round(float(np.median(rt[:, 7] - rt[:, 0])), 2),
+                "clock_ghz_median": round(float(np.median(clk)), 2)})
+        print(cfg, json.dumps(res[-1]))
+        print(cfg, "spans", [r["span_us"] for r in res])
+        del env
+
+
+if __name__ == "__main__":
+    main()
