@@ -6,20 +6,25 @@
 // terminal logic, the masked re-initialisation of finished envs and the
 // recomputed observations of those envs.
 //
-// Mapping: a workgroup owns a tile of E consecutive envs and
-// runs one lane per agent row (R = E*A lanes, env-major, so lane t owns row
-// e0*A + t of the (P*A, .) agent arrays). The tile's array-of-structs inputs
-// (states 5A floats/env, obstacles 2S, target 2) are staged in LDS with
-// 16-byte coalesced loads; the packed observation tile (A*D floats/env) is
-// assembled in LDS and streamed out with 16-byte coalesced stores. Per-env
-// reductions over agents go through LDS. No MFMA: nothing here contracts.
+// Mapping. The unit of work is a wave tile: W consecutive envs
+// (W = 64 / A rounded down to a multiple of 4 where possible: 20 envs at
+// A = 3) handled by ONE wavefront, one lane per agent row, env-major, so lane
+// t owns row e0*A + t of the (P*A, .) agent arrays. Every wave works alone:
+// it stages its tile's array-of-structs inputs in a wave-private LDS slice
+// with 16-byte coalesced loads (all issued before the first wait), exchanges
+// rows through that slice with wave-scope ordering only, and streams the
+// packed observation tile back out with 16-byte stores. There is no
+// __syncthreads() and no inter-wave dependency, so the waves of a CU drift
+// apart and overlap each other's memory and VALU phases. Large batches loop
+// over tiles with a grid-stride (persistent waves). No MFMA: nothing here
+// contracts.
 //
 // Numerics: built with -ffp-contract=off and the HIP default
 // correctly rounded fp32 division and sqrt, so every distance, dot product
-// and reward term is the same fp32 expression the reference's CPU path
-// evaluates. The heading rotation evaluates sin/cos in double and rounds once
-// (see oracle/marlnav_oracle.c for the identical CPU recipe); acos is the
-// device libm's acosf.
+// and reward term is the fp32 expression the reference's CPU path evaluates,
+// summed in torch's order. sin/cos of the heading update are evaluated in
+// double (sincos_k, identical code in oracle/marlnav_oracle.c) and rounded
+// once; acos is the device libm's acosf.
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -32,17 +37,23 @@
 namespace {
 
 constexpr float kPiF = 3.14159265358979323846f;
+constexpr int kMaxAgents = 64;
+constexpr int kMaxStride = 256;
+constexpr int kWavesPerBlock = 4;
+constexpr int kWaveLdsFloats = 4096;    // 16 KiB per wave, 64 KiB per block
+constexpr int kObsTileMax = 2304;       // floats of packed obs staged per wave
+constexpr int64_t kMaxWaves = 256 * 32; // persistent cap: 32 waves per CU
 
 // Timing-only ablation builds (scripts/kbench.py; never shipped, results
-// wrong by construction): 1 no acos, 2 fast fp32 sin/cos, 4 fast division,
+// wrong by construction): 1 no acos, 2 fp32 fast sin/cos, 4 fast division,
 // 8 fast sqrt, 16 no observation math at all.
 #ifndef MARLNAV_ABLATE
 #define MARLNAV_ABLATE 0
 #endif
 
 // Diagnostic build (MARLNAV_STAMPS=1, scripts/kstamps.py): lane 0 of every
-// block records s_memrealtime / s_memtime at each phase boundary into a
-// buffer registered with marlnav_debug_stamps(). Never in the shipped build.
+// wave records s_memrealtime / s_memtime at each phase boundary of its first
+// tile into a buffer registered with marlnav_debug_stamps().
 #ifndef MARLNAV_STAMPS
 #define MARLNAV_STAMPS 0
 #endif
@@ -50,8 +61,8 @@ constexpr float kPiF = 3.14159265358979323846f;
 __device__ unsigned long long *g_stamps;
 #define STAMP(k)                                                                   \
     do {                                                                           \
-        if (threadIdx.x == 0) {                                                    \
-            unsigned long long *sp_ = g_stamps + (size_t)blockIdx.x * 16;          \
+        if (lane == 0 && first) {                                                  \
+            unsigned long long *sp_ = g_stamps + (size_t)gw * 16;                  \
             sp_[2 * (k)] = wall_clock64();                                         \
             sp_[2 * (k) + 1] = clock64();                                          \
         }                                                                          \
@@ -61,9 +72,6 @@ __device__ unsigned long long *g_stamps;
     do {         \
     } while (0)
 #endif
-constexpr int kMaxAgents = 64;
-constexpr int kMaxStride = 256;
-constexpr int kLdsBudget = 48 * 1024;
 
 thread_local char g_err[512] = "";
 
@@ -119,15 +127,38 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
     return dist < cap ? 0.0f : ang;
 }
 
-__device__ __forceinline__ void sincos_rn(float th, float *s, float *c)
+// sin/cos of an angle already clamped to [-pi, pi], evaluated in double and
+// rounded once: Cody-Waite reduction by pi/2 (two-part constant, |k| <= 2)
+// and the fdlibm __kernel_sin/__kernel_cos minimax polynomials on
+// [-pi/4, pi/4]. Identical expression tree in oracle/marlnav_oracle.c.
+__device__ __forceinline__ void sincos_k(float th, float *s_out, float *c_out)
 {
 #if MARLNAV_ABLATE & 2
-    __sincosf(th, s, c);
+    __sincosf(th, s_out, c_out);
 #else
-    double sd, cd;
-    sincos((double)th, &sd, &cd);
-    *s = (float)sd;
-    *c = (float)cd;
+    const double x = (double)th;
+    const double k = __builtin_rint(x * 6.36619772367581382433e-01);
+    double r = __builtin_fma(-k, 1.57079632679489655800e+00, x);
+    r = __builtin_fma(-k, 6.12323399573676603587e-17, r);
+    r = k == 0.0 ? x : r;  // keeps the sign of -0
+    const double z = r * r;
+    double ps = __builtin_fma(1.58969099521155010221e-10, z, -2.50507602534068634195e-08);
+    ps = __builtin_fma(ps, z, 2.75573137070700676789e-06);
+    ps = __builtin_fma(ps, z, -1.98412698298579493134e-04);
+    ps = __builtin_fma(ps, z, 8.33333333332248946124e-03);
+    ps = __builtin_fma(ps, z, -1.66666666666666324348e-01);
+    const double sn = r == 0.0 ? r : __builtin_fma(r * z, ps, r);  // sin(-0) = -0
+    double pc = __builtin_fma(-1.13596475577881948265e-11, z, 2.08757232129817482790e-09);
+    pc = __builtin_fma(pc, z, -2.75573143513906633035e-07);
+    pc = __builtin_fma(pc, z, 2.48015872894767294178e-05);
+    pc = __builtin_fma(pc, z, -1.38888888888741095749e-03);
+    pc = __builtin_fma(pc, z, 4.16666666666666019037e-02);
+    const double cs = __builtin_fma(z * z, pc, __builtin_fma(-0.5, z, 1.0));
+    const int q = ((int)k) & 3;
+    const double s = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
+    const double c = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
+    *s_out = (float)s;
+    *c_out = (float)c;
 #endif
 }
 
@@ -186,123 +217,11 @@ __device__ void native_fresh_env(int A, int S, const MarlnavParams &pr,
             s[0] = s[0] + pr.ags_dist * (pr.noise_std * z0);
             s[1] = s[1] + pr.ags_dist * (pr.noise_std * z1);
             float sn, c;
-            sincos_rn(pr.angle_range * (u3 - 0.5f), &sn, &c);
+            sincos_k(pr.angle_range * (u3 - 0.5f), &sn, &c);
             const float dx = s[2], dy = s[3];
             s[2] = c * dx + (-sn) * dy;
             s[3] = sn * dx + c * dy;
         }
-    }
-}
-
-// ------------------------------------------------------------ tile copies
-// Cooperative contiguous copy of n floats, 16-byte vectors where both sides
-// allow it. LDS destinations are 16-byte aligned by construction.
-__device__ __forceinline__ void tile_load(float *__restrict__ dst, const float *__restrict__ src,
-                                          int n, int tid, int nthr)
-{
-    int head = 0;
-    if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
-        const int n4 = n >> 2;
-        const float4 *s4 = reinterpret_cast<const float4 *>(src);
-        float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int i = tid; i < n4; i += nthr) d4[i] = s4[i];
-        head = n4 << 2;
-    }
-    for (int i = head + tid; i < n; i += nthr) dst[i] = src[i];
-}
-
-__device__ __forceinline__ void tile_store(float *__restrict__ dst, const float *__restrict__ src,
-                                           int n, int tid, int nthr)
-{
-    int head = 0;
-    if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
-        const int n4 = n >> 2;
-        const float4 *s4 = reinterpret_cast<const float4 *>(src);
-        float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int i = tid; i < n4; i += nthr) d4[i] = s4[i];
-        head = n4 << 2;
-    }
-    for (int i = head + tid; i < n; i += nthr) dst[i] = src[i];
-}
-
-// Stage three contiguous global ranges into LDS with every global load of
-// the tile issued before the first wait: up to KMAX 16-byte vectors per
-// lane are held in registers, then written to LDS. (A load -> LDS-store ->
-// next-load loop would pay one full memory round trip per iteration.)
-struct Span {
-    const float *src;
-    float *dst;
-    int n;  // floats
-};
-
-template <int KMAX>
-__device__ __forceinline__ void stage_spans(Span a, Span b, Span c, int tid, int nthr)
-{
-    const bool vec = ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(b.src) |
-                       reinterpret_cast<uintptr_t>(c.src)) & 15u) == 0 && nthr >= 12;
-    if (!vec) {  // unaligned shard base: plain scalar staging
-        tile_load(a.dst, a.src, a.n, tid, nthr);
-        tile_load(b.dst, b.src, b.n, tid, nthr);
-        tile_load(c.dst, c.src, c.n, tid, nthr);
-        return;
-    }
-    const int va = a.n >> 2, vb = b.n >> 2, vc = c.n >> 2;
-    const int vt = va + vb + vc;
-    float4 r[KMAX];
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-        const int i = tid + k * nthr;
-        if (i < vt) {
-            const float *p = i < va ? a.src + 4 * i
-                                    : (i < va + vb ? b.src + 4 * (i - va) : c.src + 4 * (i - va - vb));
-            r[k] = *reinterpret_cast<const float4 *>(p);
-        }
-    }
-    // scalar tails (< 4 floats per span), one lane per float
-    float t = 0.0f;
-    const int ta = a.n & 3, tb = b.n & 3, tc = c.n & 3;
-    const int lane_t = tid - (nthr - 12);  // last 12 lanes take the tails
-    const float *tsrc = nullptr;
-    float *tdst = nullptr;
-    if (lane_t >= 0) {
-        const int j = lane_t & 3, w = lane_t >> 2;
-        const Span &sp = w == 0 ? a : (w == 1 ? b : c);
-        const int tn = w == 0 ? ta : (w == 1 ? tb : tc);
-        if (j < tn) {
-            tsrc = sp.src + (sp.n & ~3) + j;
-            tdst = sp.dst + (sp.n & ~3) + j;
-            t = *tsrc;
-        }
-    }
-    // generic tiles with more vectors than KMAX per lane
-    for (int i = tid + KMAX * nthr; i < vt; i += nthr) {
-        const float *p = i < va ? a.src + 4 * i
-                                : (i < va + vb ? b.src + 4 * (i - va) : c.src + 4 * (i - va - vb));
-        float *q = i < va ? a.dst + 4 * i
-                          : (i < va + vb ? b.dst + 4 * (i - va) : c.dst + 4 * (i - va - vb));
-        *reinterpret_cast<float4 *>(q) = *reinterpret_cast<const float4 *>(p);
-    }
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-        const int i = tid + k * nthr;
-        if (i < vt) {
-            float *q = i < va ? a.dst + 4 * i
-                              : (i < va + vb ? b.dst + 4 * (i - va) : c.dst + 4 * (i - va - vb));
-            *reinterpret_cast<float4 *>(q) = r[k];
-        }
-    }
-    if (tdst) *tdst = t;
-}
-
-// ObsNormalizer fused into the store (utils.py:530-532)
-__device__ __forceinline__ void tile_store_norm(float *__restrict__ dst,
-                                                const float *__restrict__ src, int n, int D,
-                                                const float *__restrict__ mean,
-                                                const float *__restrict__ scale, int tid, int nthr)
-{
-    for (int i = tid; i < n; i += nthr) {
-        const int k = i % D;
-        dst[i] = (src[i] - mean[k]) / scale[k];
     }
 }
 
@@ -352,6 +271,118 @@ __device__ __forceinline__ float torch_row_sum(const float *x, int n, F f)
     return a0;
 }
 
+// Make LDS writes of some lanes visible to later LDS reads of other lanes of
+// the SAME wave: the LDS executes one wave's requests in issue order, so only
+// the compiler must be kept from reordering across this point.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ------------------------------------------------------------ wave staging
+// Copy three contiguous global ranges into the wave's LDS slice with every
+// global load issued before the first wait (a load -> LDS-store -> load loop
+// would pay one memory round trip per iteration).
+struct Span {
+    const float *src;
+    float *dst;
+    int n;  // floats
+};
+
+__device__ __forceinline__ const float *span_src(const Span &a, const Span &b, const Span &c,
+                                                 int i, int na, int nb)
+{
+    return i < na ? a.src + i : (i < na + nb ? b.src + (i - na) : c.src + (i - na - nb));
+}
+
+__device__ __forceinline__ float *span_dst(const Span &a, const Span &b, const Span &c, int i,
+                                           int na, int nb)
+{
+    return i < na ? a.dst + i : (i < na + nb ? b.dst + (i - na) : c.dst + (i - na - nb));
+}
+
+template <int KMAX>
+__device__ __forceinline__ void stage_spans(Span a, Span b, Span c, int lane)
+{
+    const bool vec = ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(b.src) |
+                       reinterpret_cast<uintptr_t>(c.src)) & 15u) == 0;
+    if (!vec) {  // unaligned tile base (tiny W): scalar loads, all in flight
+        float r0[4 * KMAX];
+        const int nt = a.n + b.n + c.n;
+#pragma unroll
+        for (int k = 0; k < 4 * KMAX; ++k) {
+            const int i = lane + 64 * k;
+            if (i < nt) r0[k] = *span_src(a, b, c, i, a.n, b.n);
+        }
+        for (int i = lane + 64 * 4 * KMAX; i < nt; i += 64)
+            *span_dst(a, b, c, i, a.n, b.n) = *span_src(a, b, c, i, a.n, b.n);
+#pragma unroll
+        for (int k = 0; k < 4 * KMAX; ++k) {
+            const int i = lane + 64 * k;
+            if (i < nt) *span_dst(a, b, c, i, a.n, b.n) = r0[k];
+        }
+        return;
+    }
+    const int va = a.n >> 2, vb = b.n >> 2, vc = c.n >> 2;
+    const int vt = va + vb + vc;
+    float4 r[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int i = lane + 64 * k;
+        if (i < vt)
+            r[k] = *reinterpret_cast<const float4 *>(span_src(a, b, c, 4 * i, 4 * va, 4 * vb));
+    }
+    // scalar tails (< 4 floats per span): lanes 52..63
+    float t = 0.0f;
+    float *tdst = nullptr;
+    const int lt = lane - 52;
+    if (lt >= 0) {
+        const int j = lt & 3, w = lt >> 2;
+        const Span &sp = w == 0 ? a : (w == 1 ? b : c);
+        if (j < (sp.n & 3)) {
+            tdst = sp.dst + (sp.n & ~3) + j;
+            t = sp.src[(sp.n & ~3) + j];
+        }
+    }
+    for (int i = lane + 64 * KMAX; i < vt; i += 64)
+        *reinterpret_cast<float4 *>(span_dst(a, b, c, 4 * i, 4 * va, 4 * vb)) =
+            *reinterpret_cast<const float4 *>(span_src(a, b, c, 4 * i, 4 * va, 4 * vb));
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int i = lane + 64 * k;
+        if (i < vt) *reinterpret_cast<float4 *>(span_dst(a, b, c, 4 * i, 4 * va, 4 * vb)) = r[k];
+    }
+    if (tdst) *tdst = t;
+}
+
+// Stream n floats of the wave's LDS slice to global memory (16-byte stores
+// when the destination allows), optionally also the ObsNormalizer output
+// (utils.py:530-532) of every element.
+__device__ __forceinline__ void wave_store(float *__restrict__ dst, const float *__restrict__ src,
+                                           int n, int lane, float *__restrict__ nrm_dst,
+                                           const float *__restrict__ mean,
+                                           const float *__restrict__ scale, int D)
+{
+    int head = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+        const int n4 = n >> 2;
+        for (int i = lane; i < n4; i += 64) {
+            const float4 v = *reinterpret_cast<const float4 *>(src + 4 * i);
+            *reinterpret_cast<float4 *>(dst + 4 * i) = v;
+        }
+        head = n4 << 2;
+    }
+    for (int i = head + lane; i < n; i += 64) dst[i] = src[i];
+    if (nrm_dst) {
+        for (int i = lane; i < n; i += 64) {
+            const int k = i % D;
+            nrm_dst[i] = (src[i] - mean[k]) / scale[k];
+        }
+    }
+}
+
 // ------------------------------------------------------------ row observe
 struct RowOut {
     float r_miss, r_hit;  // agent reward if the env misses / reaches the target
@@ -360,6 +391,7 @@ struct RowOut {
 
 // observations() for agent row `a` of one env (environment.py:139-180), with
 // the per-agent reward terms of _rews_and_terms (:184-269) when TERMS.
+// `row` is the packed output row (LDS or global, stride 1).
 template <int A_T, int O_T, bool TERMS>
 __device__ __forceinline__ RowOut observe_row(int Arun, int Orun, const float *__restrict__ sts,
                                               const float *__restrict__ obe,
@@ -443,37 +475,33 @@ __device__ __forceinline__ RowOut observe_row(int Arun, int Orun, const float *_
 }
 
 // -------------------------------------------------------------- LDS plan
-struct TilePlan {
-    int E, R, A, O, S, D;
-    int off_st, off_ob, off_tg, off_obs, off_rm, off_rh, off_fl, off_env, off_cnt, off_nm,
-        off_ns;
-    int bytes;
+// Per-wave LDS slice, in floats, identical on host and device.
+struct WavePlan {
+    int W, A, O, S, D, obs_lds;
+    int off_st, off_ob, off_tg, off_obs, off_rm, off_rh, off_fl, off_env, floats;
 };
 
 __host__ __device__ inline int align4(int n) { return (n + 3) & ~3; }  // floats -> 16 B
 
-__host__ __device__ inline TilePlan make_plan(int E, int A, int O, int S)
+__host__ __device__ inline WavePlan make_plan(int W, int A, int O, int S)
 {
-    TilePlan p;
-    p.E = E;
+    WavePlan p;
+    p.W = W;
     p.A = A;
     p.O = O;
     p.S = S;
-    p.R = E * A;
     p.D = obs_dim(A, O);
+    p.obs_lds = W * A * p.D <= kObsTileMax;
     int o = 0;
-    p.off_st = o;  o += align4(p.R * 5);
-    p.off_ob = o;  o += align4(E * S * 2);
-    p.off_tg = o;  o += align4(E * 2);
-    p.off_obs = o; o += align4(p.R * p.D);
-    p.off_rm = o;  o += align4(p.R);
-    p.off_rh = o;  o += align4(p.R);
-    p.off_fl = o;  o += align4(p.R);
-    p.off_env = o; o += align4(E);
-    p.off_cnt = o; o += 4;
-    p.off_nm = o;  o += align4(p.D);
-    p.off_ns = o;  o += align4(p.D);
-    p.bytes = o * 4;
+    p.off_st = o;  o += align4(W * A * 5);
+    p.off_ob = o;  o += align4(W * S * 2);
+    p.off_tg = o;  o += align4(W * 2);
+    p.off_obs = o; o += p.obs_lds ? align4(W * A * p.D) : 0;
+    p.off_rm = o;  o += 64;
+    p.off_rh = o;  o += 64;
+    p.off_fl = o;  o += 64;
+    p.off_env = o; o += 64;
+    p.floats = o;
     return p;
 }
 
@@ -481,207 +509,191 @@ struct StepArgs {
     MarlnavStepBuffers b;
     int64_t P;
     int64_t env_offset;
-    int64_t slots;
+    int64_t ntiles;
+    int64_t waves;     // waves in the grid (= counter slots)
     uint64_t step_idx;
-    int E, A, O, S;
+    int W, A, O, S;
 };
 
-// env-level bits kept in LDS between phases
-constexpr unsigned kFin = 1u;
-
 // --------------------------------------------------------------- step kernel
-template <int A_T, int O_T>
-__global__ void __launch_bounds__(1024) step_kernel(StepArgs args, MarlnavParams pr)
+template <int A_T, int O_T, bool OBS_ONLY>
+__global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args, MarlnavParams pr)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int A = A_T ? A_T : args.A;
     const int O = O_T ? O_T : args.O;
-    const int S = args.S;
-    const TilePlan tp = make_plan(args.E, A, O, S);
-    const int E = tp.E, D = tp.D;
-    const int tid = threadIdx.x, nthr = blockDim.x;
-    const int64_t e0 = (int64_t)blockIdx.x * E;
-    const int ne = (int)((args.P - e0) < E ? (args.P - e0) : E);
-    const int nr = ne * A;
-
-    float *st = lds + tp.off_st;
-    float *ob = lds + tp.off_ob;
-    float *tg = lds + tp.off_tg;
-    float *obs = lds + tp.off_obs;
-    float *rmiss = lds + tp.off_rm;
-    float *rhit = lds + tp.off_rh;
-    unsigned *rfl = reinterpret_cast<unsigned *>(lds + tp.off_fl);
-    unsigned *envbits = reinterpret_cast<unsigned *>(lds + tp.off_env);
-    unsigned *cnt = reinterpret_cast<unsigned *>(lds + tp.off_cnt);
+    const int S = args.S, W = args.W;
+    const WavePlan wp = make_plan(W, A, O, S);
+    const int D = wp.D;
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wib;
+    float *wl = lds + wib * wp.floats;
+    float *st = wl + wp.off_st;
+    float *ob = wl + wp.off_ob;
+    float *tg = wl + wp.off_tg;
+    float *obs_t = wl + wp.off_obs;
+    float *rmiss = wl + wp.off_rm;
+    float *rhit = wl + wp.off_rh;
+    unsigned *rfl = reinterpret_cast<unsigned *>(wl + wp.off_fl);
+    unsigned *envbits = reinterpret_cast<unsigned *>(wl + wp.off_env);
     const MarlnavStepBuffers &b = args.b;
-    const bool norm = (pr.flags & MARLNAV_WRITE_OBS_NORM) != 0;
-
-    STAMP(0);
-    // ---- phase 0: stage the tile (all global loads in flight together)
-    float2 act = make_float2(0.0f, 0.0f);
-    if (tid < nr) act = reinterpret_cast<const float2 *>(b.actions)[e0 * A + tid];
-    float step_num_in = 0.0f;
-    uint8_t term_in = 0;
-    if (tid < ne) {
-        step_num_in = b.step_num[e0 + tid];
-        term_in = b.terminates[e0 + tid];
-    }
-    stage_spans<4>(Span{b.states + e0 * A * 5, st, nr * 5},
-                   Span{b.obstacles + e0 * S * 2, ob, ne * S * 2},
-                   Span{b.target + e0 * 2, tg, ne * 2}, tid, nthr);
-    if (norm) {
-        for (int k = tid; k < D; k += nthr) {
-            lds[tp.off_nm + k] = b.norm_mean[k];
-            lds[tp.off_ns + k] = b.norm_scale[k];
-        }
-    }
-    if (tid < 3) cnt[tid] = 0u;
-    __syncthreads();
-    STAMP(1);
-
-    // ---- phase 1: _move_agents (environment.py:113-123)
-    const int el = tid / A, a = tid - el * A;
-    if (tid < nr) {
-        float a0 = act.x, a1 = act.y;
-        if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
-            a0 = pr.act_scale[0] * a0 + pr.act_mean[0];
-            a1 = pr.act_scale[1] * a1 + pr.act_mean[1];
-        }
-        float *s = st + 5 * tid;
-        float sn, c;
-        sincos_rn(clamp_t(a0, -kPiF, kPiF), &sn, &c);
-        const float dx = s[2], dy = s[3];
-        const float ndx = c * dx + (-sn) * dy;
-        const float ndy = sn * dx + c * dy;
-        const float v = clamp_t(s[4] + clamp_t(a1, pr.min_accel, pr.max_accel), pr.min_speed,
-                                pr.max_speed);
-        s[0] = s[0] + ndx * v;
-        s[1] = s[1] + ndy * v;
-        s[2] = ndx;
-        s[3] = ndy;
-        s[4] = v;
-    }
-    __syncthreads();
-    STAMP(2);
-
-    // ---- phase 2: observations of the moved state + reward terms (:99-100)
-    if (tid < nr && !(MARLNAV_ABLATE & 16)) {
-        const RowOut ro = observe_row<A_T, O_T, true>(A, O, st + 5 * A * el, ob + 2 * S * el,
-                                                      tg + 2 * el, a, obs + tid * D, pr);
-        rmiss[tid] = ro.r_miss;
-        rhit[tid] = ro.r_hit;
-        rfl[tid] = ro.flags;
-    }
-    __syncthreads();
-    STAMP(3);
-
-    // ---- phase 3: per-env reductions, terminal logic, masked re-init
-    if (tid < ne) {
-        const int64_t e = e0 + tid;
-        unsigned any_col = 0u, all_in = 1u;
-        for (int i = 0; i < A; ++i) {
-            const unsigned f = rfl[tid * A + i];
-            any_col |= f & 1u;
-            all_in &= (f >> 1) & 1u;
-        }
-        const float *rr = all_in ? rhit : rmiss;
-        const float rsum = torch_row_sum(rr + tid * A, A, [](float r) { return r; });
-        b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
-
-        float step_num = step_num_in + 1.0f;               // :96
-        const bool truncated = step_num > pr.trunc_after;  // :97
-        const bool term_old = term_in != 0;
-        const bool terminated = any_col || term_old;       // :213-214
-        b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
-        b.terminated[e] = (uint8_t)terminated;
-        b.truncated[e] = (uint8_t)truncated;
-        if (truncated) atomicAdd(&cnt[0], 1u);
-        if (any_col) atomicAdd(&cnt[1], 1u);
-        if (all_in) atomicAdd(&cnt[2], 1u);
-
-        unsigned bits = 0u;
-        if (truncated || terminated) {                     // :102-104
-            bits = kFin;
-            float *sts = st + 5 * A * tid;
-            float *obe = ob + 2 * S * tid;
-            float *tge = tg + 2 * tid;
-            if (b.fresh_states) {
-                if (!(pr.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
-                    for (int i = 0; i < 5 * A; ++i) sts[i] = b.fresh_states[e * A * 5 + i];
-                for (int i = 0; i < 2 * S; ++i) obe[i] = b.fresh_obstacles[e * S * 2 + i];
-                tge[0] = b.fresh_target[2 * e];
-                tge[1] = b.fresh_target[2 * e + 1];
-            } else {
-                native_fresh_env(A, S, pr, b.formation, (uint64_t)(args.env_offset + e),
-                                 args.step_idx, sts, obe, tge);
-            }
-            for (int i = 0; i < 2 * S; ++i) b.obstacles[e * S * 2 + i] = obe[i];
-            b.target[2 * e] = tge[0];
-            b.target[2 * e + 1] = tge[1];
-            step_num = 0.0f;
-        }
-        b.step_num[e] = step_num;
-        envbits[tid] = bits;
-    }
-    __syncthreads();
-    STAMP(4);
-
-    // ---- phase 4: observations of re-initialised envs (:105)
-    if (tid < nr && (envbits[el] & kFin)) {
-        observe_row<A_T, O_T, false>(A, O, st + 5 * A * el, ob + 2 * S * el, tg + 2 * el, a,
-                                     obs + tid * D, pr);
-    }
-    __syncthreads();
-    STAMP(5);
-
-    // ---- phase 5: stream the tile out
-    tile_store(b.states + e0 * A * 5, st, nr * 5, tid, nthr);
-    tile_store(b.obs + e0 * A * D, obs, nr * D, tid, nthr);
-    if (norm)
-        tile_store_norm(b.obs_norm + e0 * A * D, obs, nr * D, D, lds + tp.off_nm,
-                        lds + tp.off_ns, tid, nthr);
-    if (tid < 3 && b.counters) {
-        const unsigned v = cnt[tid];
-        if (v) b.counters[tid * args.slots + blockIdx.x] += v;
-    }
-    STAMP(6);
+    const bool norm = !OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM) != 0;
+    const int el = lane / A, a = lane - el * A;
+    unsigned c_trunc = 0, c_col = 0, c_tar = 0;
 #if MARLNAV_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    STAMP(7);
+    bool first = true;
 #endif
-}
 
-// ------------------------------------------------------------ observe kernel
-template <int A_T, int O_T>
-__global__ void __launch_bounds__(1024) observe_kernel(StepArgs args)
-{
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int A = A_T ? A_T : args.A;
-    const int O = O_T ? O_T : args.O;
-    const int S = args.S;
-    const TilePlan tp = make_plan(args.E, A, O, S);
-    const int E = tp.E, D = tp.D;
-    const int tid = threadIdx.x, nthr = blockDim.x;
-    const int64_t e0 = (int64_t)blockIdx.x * E;
-    const int ne = (int)((args.P - e0) < E ? (args.P - e0) : E);
-    const int nr = ne * A;
-    float *st = lds + tp.off_st;
-    float *ob = lds + tp.off_ob;
-    float *tg = lds + tp.off_tg;
-    float *obs = lds + tp.off_obs;
-    stage_spans<4>(Span{args.b.states + e0 * A * 5, st, nr * 5},
-                   Span{args.b.obstacles + e0 * S * 2, ob, ne * S * 2},
-                   Span{args.b.target + e0 * 2, tg, ne * 2}, tid, nthr);
-    __syncthreads();
-    if (tid < nr) {
-        const int el = tid / A, a = tid - el * A;
-        MarlnavParams pr{};
-        pr.cap_distance = 0.1f;
-        observe_row<A_T, O_T, false>(A, O, st + 5 * A * el, ob + 2 * S * el, tg + 2 * el, a,
-                                     obs + tid * D, pr);
+    for (int64_t tile = gw; tile < args.ntiles; tile += args.waves) {
+        STAMP(0);
+        const int64_t e0 = tile * W;
+        const int ne = (int)((args.P - e0) < W ? (args.P - e0) : W);
+        const int nr = ne * A;
+        const bool row_on = lane < nr;
+        const bool env_on = lane < ne;
+
+        // ---- stage the tile; every global load in flight before any wait
+        float2 act = make_float2(0.0f, 0.0f);
+        float step_num_in = 0.0f;
+        uint8_t term_in = 0;
+        if (!OBS_ONLY) {
+            if (row_on) act = reinterpret_cast<const float2 *>(b.actions)[e0 * A + lane];
+            if (env_on) {
+                step_num_in = b.step_num[e0 + lane];
+                term_in = b.terminates[e0 + lane];
+            }
+        }
+        stage_spans<4>(Span{b.states + e0 * A * 5, st, nr * 5},
+                       Span{b.obstacles + e0 * S * 2, ob, ne * S * 2},
+                       Span{b.target + e0 * 2, tg, ne * 2}, lane);
+        wave_sync();
+        STAMP(1);
+
+        // ---- _move_agents (environment.py:113-123), own row only
+        if (!OBS_ONLY && row_on) {
+            float a0 = act.x, a1 = act.y;
+            if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
+                a0 = pr.act_scale[0] * a0 + pr.act_mean[0];
+                a1 = pr.act_scale[1] * a1 + pr.act_mean[1];
+            }
+            float *s = st + 5 * lane;
+            float sn, c;
+            sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+            const float dx = s[2], dy = s[3];
+            const float ndx = c * dx + (-sn) * dy;
+            const float ndy = sn * dx + c * dy;
+            const float v = clamp_t(s[4] + clamp_t(a1, pr.min_accel, pr.max_accel),
+                                    pr.min_speed, pr.max_speed);
+            s[0] = s[0] + ndx * v;
+            s[1] = s[1] + ndy * v;
+            s[2] = ndx;
+            s[3] = ndy;
+            s[4] = v;
+        }
+        wave_sync();
+        STAMP(2);
+
+        // ---- observations of the moved state + reward terms (:99-100)
+        float *out_row = wp.obs_lds ? obs_t + lane * D : b.obs + (e0 * A + lane) * D;
+        if (row_on && !(MARLNAV_ABLATE & 16)) {
+            const RowOut ro = observe_row<A_T, O_T, !OBS_ONLY>(
+                A, O, st + 5 * A * el, ob + 2 * S * el, tg + 2 * el, a, out_row, pr);
+            if (!OBS_ONLY) {
+                rmiss[lane] = ro.r_miss;
+                rhit[lane] = ro.r_hit;
+                rfl[lane] = ro.flags;
+            }
+        }
+        wave_sync();
+        STAMP(3);
+
+        if (!OBS_ONLY) {
+            // ---- per-env reductions, terminal logic, masked re-init
+            bool fin = false;
+            if (env_on) {
+                const int64_t e = e0 + lane;
+                unsigned any_col = 0u, all_in = 1u;
+                for (int i = 0; i < A; ++i) {
+                    const unsigned f = rfl[lane * A + i];
+                    any_col |= f & 1u;
+                    all_in &= (f >> 1) & 1u;
+                }
+                const float *rr = all_in ? rhit : rmiss;
+                const float rsum = torch_row_sum(rr + lane * A, A, [](float r) { return r; });
+                b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
+
+                float step_num = step_num_in + 1.0f;               // :96
+                const bool truncated = step_num > pr.trunc_after;  // :97
+                const bool term_old = term_in != 0;
+                const bool terminated = any_col || term_old;       // :213-214
+                b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
+                b.terminated[e] = (uint8_t)terminated;
+                b.truncated[e] = (uint8_t)truncated;
+                c_trunc += truncated;
+                c_col += any_col;
+                c_tar += all_in;
+                fin = truncated || terminated;                     // :102-104
+                if (fin) {
+                    float *sts = st + 5 * A * lane;
+                    float *obe = ob + 2 * S * lane;
+                    float *tge = tg + 2 * lane;
+                    if (b.fresh_states) {
+                        if (!(pr.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
+                            for (int i = 0; i < 5 * A; ++i) sts[i] = b.fresh_states[e * A * 5 + i];
+                        for (int i = 0; i < 2 * S; ++i) obe[i] = b.fresh_obstacles[e * S * 2 + i];
+                        tge[0] = b.fresh_target[2 * e];
+                        tge[1] = b.fresh_target[2 * e + 1];
+                    } else {
+                        native_fresh_env(A, S, pr, b.formation, (uint64_t)(args.env_offset + e),
+                                         args.step_idx, sts, obe, tge);
+                    }
+                    for (int i = 0; i < 2 * S; ++i) b.obstacles[e * S * 2 + i] = obe[i];
+                    b.target[2 * e] = tge[0];
+                    b.target[2 * e + 1] = tge[1];
+                    step_num = 0.0f;
+                }
+                b.step_num[e] = step_num;
+                envbits[lane] = fin ? 1u : 0u;
+            }
+            const bool any_fin = __ballot(fin) != 0ull;
+            wave_sync();
+            STAMP(4);
+
+            // ---- observations of re-initialised envs (:105)
+            if (any_fin) {
+                if (row_on && envbits[el])
+                    observe_row<A_T, O_T, false>(A, O, st + 5 * A * el, ob + 2 * S * el,
+                                                 tg + 2 * el, a, out_row, pr);
+                wave_sync();
+            }
+            STAMP(5);
+        }
+
+        // ---- stream the tile out
+        if (wp.obs_lds)
+            wave_store(b.obs + e0 * A * D, obs_t, nr * D, lane,
+                       norm ? b.obs_norm + e0 * A * D : nullptr, b.norm_mean, b.norm_scale, D);
+        else if (norm && row_on)
+            for (int k = 0; k < D; ++k)
+                b.obs_norm[(e0 * A + lane) * D + k] =
+                    (out_row[k] - b.norm_mean[k]) / b.norm_scale[k];
+        if (!OBS_ONLY)
+            wave_store(b.states + e0 * A * 5, st, nr * 5, lane, nullptr, nullptr, nullptr, 1);
+        STAMP(6);
+#if MARLNAV_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(7);
+        first = false;
+#endif
+        wave_sync();  // the next tile overwrites this slice
     }
-    __syncthreads();
-    tile_store(args.b.obs + e0 * A * D, obs, nr * D, tid, nthr);
+    if (!OBS_ONLY && b.counters && lane == 0) {
+        // this wave's own slots: contention-free, fire-and-forget
+        if (c_trunc) atomicAdd(&b.counters[0 * args.waves + gw], (unsigned long long)c_trunc);
+        if (c_col) atomicAdd(&b.counters[1 * args.waves + gw], (unsigned long long)c_col);
+        if (c_tar) atomicAdd(&b.counters[2 * args.waves + gw], (unsigned long long)c_tar);
+    }
 }
 
 // ----------------------------------------------------- native reinit kernel
@@ -708,17 +720,39 @@ __global__ void counters_total_kernel(const uint64_t *__restrict__ c, int64_t sl
 }
 
 // ------------------------------------------------------------------ host
-int pick_envs_per_tile(int A, int O, int S)
+struct Launch {
+    int W;
+    int64_t ntiles, waves, blocks;
+    WavePlan plan;
+};
+
+// envs per wave tile: 64 / A, rounded down to a multiple of 4 when that
+// leaves >= 4 (16-byte aligned tiles), then shrunk to the LDS budget
+int pick_wave_envs(int A, int O, int S)
 {
-    int E = 64;
-    while (E > 1 && (E * A > 1024 || make_plan(E, A, O, S).bytes > kLdsBudget)) E >>= 1;
-    return E;
+    int W = 64 / A;
+    if (W >= 4) W &= ~3;
+    while (W > 1 && make_plan(W, A, O, S).floats > kWaveLdsFloats) W >>= 1;
+    return W < 1 ? 1 : W;
+}
+
+Launch plan_launch(const MarlnavDims *d)
+{
+    Launch L;
+    L.W = pick_wave_envs(d->num_agents, d->num_obstacles, d->obstacle_stride);
+    L.plan = make_plan(L.W, d->num_agents, d->num_obstacles, d->obstacle_stride);
+    L.ntiles = (d->num_parallel + L.W - 1) / L.W;
+    L.waves = L.ntiles < kMaxWaves ? L.ntiles : kMaxWaves;
+    L.waves = (L.waves + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+    L.blocks = L.waves / kWavesPerBlock;
+    return L;
 }
 
 int validate(const MarlnavDims *d)
 {
     if (!d) return fail(MARLNAV_EINVAL, "dims is NULL");
-    if (d->num_parallel < 1) return fail(MARLNAV_EINVAL, "num_parallel=%lld < 1", (long long)d->num_parallel);
+    if (d->num_parallel < 1)
+        return fail(MARLNAV_EINVAL, "num_parallel=%lld < 1", (long long)d->num_parallel);
     if (d->num_agents < 2 || d->num_agents > kMaxAgents)
         return fail(MARLNAV_EINVAL, "num_agents=%d outside [2, %d]", d->num_agents, kMaxAgents);
     if (d->num_obstacles < 1 || d->num_obstacles > d->obstacle_stride)
@@ -726,56 +760,60 @@ int validate(const MarlnavDims *d)
                     d->num_obstacles, d->obstacle_stride);
     if (d->obstacle_stride > kMaxStride)
         return fail(MARLNAV_EINVAL, "obstacle_stride=%d > %d", d->obstacle_stride, kMaxStride);
-    const int E = pick_envs_per_tile(d->num_agents, d->num_obstacles, d->obstacle_stride);
-    if (make_plan(E, d->num_agents, d->num_obstacles, d->obstacle_stride).bytes > 64 * 1024)
-        return fail(MARLNAV_EUNSUPPORTED, "tile does not fit LDS for A=%d O=%d S=%d",
+    const Launch L = plan_launch(d);
+    if (L.plan.floats > kWaveLdsFloats)
+        return fail(MARLNAV_EUNSUPPORTED, "wave tile does not fit LDS for A=%d O=%d S=%d",
                     d->num_agents, d->num_obstacles, d->obstacle_stride);
     return 0;
 }
 
 using StepFn = void (*)(StepArgs, MarlnavParams);
-using ObsFn = void (*)(StepArgs);
 
 struct KernelPair {
     int A, O;
-    StepFn step;
-    ObsFn obs;
+    StepFn step, obs;
 };
 
 const KernelPair kVariants[] = {
-    {3, 3, step_kernel<3, 3>, observe_kernel<3, 3>},
-    {3, 8, step_kernel<3, 8>, observe_kernel<3, 8>},
-    {3, 1, step_kernel<3, 1>, observe_kernel<3, 1>},
-    {2, 1, step_kernel<2, 1>, observe_kernel<2, 1>},
-    {16, 32, step_kernel<16, 32>, observe_kernel<16, 32>},
+    {3, 3, wave_kernel<3, 3, false>, wave_kernel<3, 3, true>},
+    {3, 8, wave_kernel<3, 8, false>, wave_kernel<3, 8, true>},
+    {3, 1, wave_kernel<3, 1, false>, wave_kernel<3, 1, true>},
+    {2, 1, wave_kernel<2, 1, false>, wave_kernel<2, 1, true>},
+    {16, 32, wave_kernel<16, 32, false>, wave_kernel<16, 32, true>},
 };
 
 KernelPair select_kernels(int A, int O)
 {
     for (const KernelPair &k : kVariants)
         if (k.A == A && k.O == O) return k;
-    return KernelPair{0, 0, step_kernel<0, 0>, observe_kernel<0, 0>};
+    return KernelPair{0, 0, wave_kernel<0, 0, false>, wave_kernel<0, 0, true>};
 }
 
-int launch_check(const char *what)
-{
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
-    return 0;
-}
-
-StepArgs make_args(const MarlnavDims *d, int E)
+StepArgs make_args(const MarlnavDims *d, const Launch &L)
 {
     StepArgs a;
     memset(&a, 0, sizeof(a));
     a.P = d->num_parallel;
     a.env_offset = d->env_offset;
-    a.E = E;
+    a.ntiles = L.ntiles;
+    a.waves = L.waves;
+    a.W = L.W;
     a.A = d->num_agents;
     a.O = d->num_obstacles;
     a.S = d->obstacle_stride;
-    a.slots = (d->num_parallel + E - 1) / E;
     return a;
+}
+
+int launch(StepFn fn, const Launch &L, StepArgs args, MarlnavParams pr, void *stream,
+           const char *what)
+{
+    void *kargs[] = {&args, &pr};
+    const size_t lds = (size_t)L.plan.floats * 4 * kWavesPerBlock;
+    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)L.blocks),
+                                   dim3(64 * kWavesPerBlock), kargs, lds, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+    return 0;
 }
 
 }  // namespace
@@ -797,8 +835,7 @@ const char *marlnav_last_error(void) { return g_err; }
 int64_t marlnav_counter_slots(const MarlnavDims *d)
 {
     if (validate(d)) return -1;
-    const int E = pick_envs_per_tile(d->num_agents, d->num_obstacles, d->obstacle_stride);
-    return (d->num_parallel + E - 1) / E;
+    return plan_launch(d).waves;
 }
 
 int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavStepBuffers *b,
@@ -817,20 +854,12 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavSte
         return fail(MARLNAV_EINVAL, "MARLNAV_WRITE_OBS_NORM needs obs_norm/norm_mean/norm_scale");
     if ((reinterpret_cast<uintptr_t>(b->actions) & 7u) != 0)
         return fail(MARLNAV_EINVAL, "actions must be 8-byte aligned");
-    const int A = d->num_agents, O = d->num_obstacles, S = d->obstacle_stride;
-    const int E = pick_envs_per_tile(A, O, S);
-    const TilePlan tp = make_plan(E, A, O, S);
-    StepArgs args = make_args(d, E);
+    const Launch L = plan_launch(d);
+    StepArgs args = make_args(d, L);
     args.b = *b;
     args.step_idx = step_idx;
-    const KernelPair k = select_kernels(A, O);
-    const dim3 grid((unsigned)args.slots), block((unsigned)tp.R);
-    MarlnavParams prv = *pr;
-    void *kargs[] = {&args, &prv};
-    const hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(k.step), grid, block,
-                                         kargs, (size_t)tp.bytes, (hipStream_t)stream);
-    if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "marlnav_step: %s", hipGetErrorString(e));
-    return launch_check("marlnav_step");
+    return launch(select_kernels(d->num_agents, d->num_obstacles).step, L, args, *pr, stream,
+                  "marlnav_step");
 }
 
 int marlnav_observe(const MarlnavDims *d, const float *states, const float *obstacles,
@@ -839,21 +868,17 @@ int marlnav_observe(const MarlnavDims *d, const float *states, const float *obst
     if (int rc = validate(d)) return rc;
     if (!states || !obstacles || !target || !obs)
         return fail(MARLNAV_EINVAL, "a required observe buffer is NULL");
-    const int A = d->num_agents, O = d->num_obstacles, S = d->obstacle_stride;
-    const int E = pick_envs_per_tile(A, O, S);
-    const TilePlan tp = make_plan(E, A, O, S);
-    StepArgs args = make_args(d, E);
+    const Launch L = plan_launch(d);
+    StepArgs args = make_args(d, L);
     args.b.states = const_cast<float *>(states);
     args.b.obstacles = const_cast<float *>(obstacles);
     args.b.target = const_cast<float *>(target);
     args.b.obs = obs;
-    const KernelPair k = select_kernels(A, O);
-    void *kargs[] = {&args};
-    const hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(k.obs),
-                                         dim3((unsigned)args.slots), dim3((unsigned)tp.R), kargs,
-                                         (size_t)tp.bytes, (hipStream_t)stream);
-    if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "marlnav_observe: %s", hipGetErrorString(e));
-    return launch_check("marlnav_observe");
+    MarlnavParams pr;
+    memset(&pr, 0, sizeof(pr));
+    pr.cap_distance = 0.1f;  // environment.py:65
+    return launch(select_kernels(d->num_agents, d->num_obstacles).obs, L, args, pr, stream,
+                  "marlnav_observe");
 }
 
 int marlnav_reinit_all(const MarlnavDims *d, const MarlnavParams *pr, const float *formation,
@@ -867,7 +892,10 @@ int marlnav_reinit_all(const MarlnavDims *d, const MarlnavParams *pr, const floa
     hipLaunchKernelGGL(reinit_all_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        d->num_parallel, d->num_agents, d->obstacle_stride, d->env_offset,
                        step_idx, *pr, formation, states, obstacles, target);
-    return launch_check("marlnav_reinit_all");
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(MARLNAV_ELAUNCH, "marlnav_reinit_all: %s", hipGetErrorString(e));
+    return 0;
 }
 
 int marlnav_counters_total(const MarlnavDims *d, const uint64_t *counters, uint64_t *out3,
@@ -878,7 +906,10 @@ int marlnav_counters_total(const MarlnavDims *d, const uint64_t *counters, uint6
     if (!counters || !out3) return fail(MARLNAV_EINVAL, "counters/out3 is NULL");
     hipLaunchKernelGGL(counters_total_kernel, dim3(3), dim3(64), 0, (hipStream_t)stream,
                        counters, slots, out3);
-    return launch_check("marlnav_counters_total");
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(MARLNAV_ELAUNCH, "marlnav_counters_total: %s", hipGetErrorString(e));
+    return 0;
 }
 
 }  // extern "C"

@@ -44,6 +44,8 @@ def load():
         lib.oracle_philox4x32_10.restype = None
         lib.oracle_normalize.argtypes = [ctypes.c_int64, ctypes.c_int, P, P, P, P]
         lib.oracle_normalize.restype = None
+        lib.oracle_sincos.argtypes = [ctypes.c_float, P, P]
+        lib.oracle_sincos.restype = None
         _lib = lib
     return _lib
 
@@ -138,6 +140,19 @@ def philox(ctr, key):
     o = np.empty(4, np.uint32)
     load().oracle_philox4x32_10(_ptr(c), _ptr(k), _ptr(o))
     return o
+
+
+def sincos(th):
+    """oracle_sincos over an array: (sin, cos) as float32 arrays."""
+    th = np.ascontiguousarray(th, np.float32).ravel()
+    s = np.empty_like(th)
+    c = np.empty_like(th)
+    lib = load()
+    sp, cp = ctypes.c_float(), ctypes.c_float()
+    for i, v in enumerate(th):
+        lib.oracle_sincos(float(v), ctypes.byref(sp), ctypes.byref(cp))
+        s[i], c[i] = sp.value, cp.value
+    return s, c
 
 
 def split_obs(obs, A, O):

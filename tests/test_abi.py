@@ -81,9 +81,10 @@ def test_validation_errors_are_loud(pkg):
     assert rc == -1 and b"NULL" in lib.marlnav_last_error()
     with pytest.raises(RuntimeError, match="NULL"):
         abi.check(rc, lib)
-    assert lib.marlnav_counter_slots(ctypes.byref(d)) == 1   # one 64-env tile
+    # one slot per wave of the grid: 20-env wave tiles at A=3, 4 waves/block
+    assert lib.marlnav_counter_slots(ctypes.byref(d)) == 4
     d.num_parallel = 65536
-    assert lib.marlnav_counter_slots(ctypes.byref(d)) == 1024
+    assert lib.marlnav_counter_slots(ctypes.byref(d)) == 3280
 
 
 def test_missing_library_is_an_error(pkg, tmp_path):

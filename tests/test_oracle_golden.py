@@ -156,3 +156,19 @@ def test_philox_known_answer():
     np.testing.assert_array_equal(
         orc.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0]),
         [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1])
+
+
+def test_oracle_sincos_is_correctly_rounded():
+    """oracle_sincos (= the kernel's sincos_k) against libm's double sin/cos
+    rounded to fp32, on random angles and the edges of [-pi, pi]."""
+    import math
+    g = np.random.default_rng(3)
+    th = np.concatenate([g.uniform(-np.pi, np.pi, 100000).astype(np.float32),
+                         np.float32([0.0, -0.0, np.pi, -np.pi, np.pi / 2, -np.pi / 2,
+                                     np.pi / 4, 1e-30, -1e-30, 1e-7])])
+    th = np.clip(th, -np.float32(np.pi), np.float32(np.pi))
+    s, c = orc.sincos(th)
+    cr_s = np.array([np.float32(math.sin(float(v))) for v in th])
+    cr_c = np.array([np.float32(math.cos(float(v))) for v in th])
+    assert (s == cr_s).mean() == 1.0 and (c == cr_c).mean() == 1.0
+    assert np.signbit(orc.sincos(np.float32([-0.0]))[0][0])  # sin(-0) = -0
