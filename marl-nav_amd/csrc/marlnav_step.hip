@@ -15,9 +15,8 @@
 // rows through that slice with wave-scope ordering only, and streams the
 // packed observation tile back out with 16-byte stores. There is no
 // __syncthreads() and no inter-wave dependency, so the waves of a CU drift
-// apart and overlap each other's memory and VALU phases. Large batches loop
-// over tiles with a grid-stride (persistent waves). No MFMA: nothing here
-// contracts.
+// apart and overlap each other's memory and VALU phases. No MFMA: nothing
+// here contracts.
 //
 // Numerics: built with -ffp-contract=off and the HIP default
 // correctly rounded fp32 division and sqrt, so every distance, dot product
@@ -42,7 +41,6 @@ constexpr int kMaxStride = 256;
 constexpr int kWavesPerBlock = 4;
 constexpr int kWaveLdsFloats = 4096;    // 16 KiB per wave, 64 KiB per block
 constexpr int kObsTileMax = 2304;       // floats of packed obs staged per wave
-constexpr int64_t kMaxWaves = 256 * 32; // persistent cap: 32 waves per CU
 
 // Timing-only ablation builds (scripts/kbench.py; never shipped, results
 // wrong by construction): 1 no acos, 2 fp32 fast sin/cos, 4 fast division,
@@ -52,8 +50,8 @@ constexpr int64_t kMaxWaves = 256 * 32; // persistent cap: 32 waves per CU
 #endif
 
 // Diagnostic build (MARLNAV_STAMPS=1, scripts/kstamps.py): lane 0 of every
-// wave records s_memrealtime / s_memtime at each phase boundary of its first
-// tile into a buffer registered with marlnav_debug_stamps().
+// wave records s_memrealtime / s_memtime at each phase boundary into a
+// buffer registered with marlnav_debug_stamps().
 #ifndef MARLNAV_STAMPS
 #define MARLNAV_STAMPS 0
 #endif
@@ -61,7 +59,7 @@ constexpr int64_t kMaxWaves = 256 * 32; // persistent cap: 32 waves per CU
 __device__ unsigned long long *g_stamps;
 #define STAMP(k)                                                                   \
     do {                                                                           \
-        if (lane == 0 && first) {                                                  \
+        if (lane == 0) {                                                           \
             unsigned long long *sp_ = g_stamps + (size_t)gw * 16;                  \
             sp_[2 * (k)] = wall_clock64();                                         \
             sp_[2 * (k) + 1] = clock64();                                          \
@@ -191,6 +189,7 @@ __device__ __forceinline__ float native_uniform(uint64_t seed, uint64_t gid, uin
 }
 
 // native TriangleIntitializer draw for one env (utils.py:375-398)
+template <bool NOISY>
 __device__ void native_fresh_env(int A, int S, const MarlnavParams &pr,
                                  const float *__restrict__ formation, uint64_t gid,
                                  uint64_t sidx, float *st, float *ob, float *tg)
@@ -204,7 +203,7 @@ __device__ void native_fresh_env(int A, int S, const MarlnavParams &pr,
     for (int i = 0; i < 5 * A; ++i) st[i] = formation[i];
     tg[0] = formation[5 * A];
     tg[1] = formation[5 * A + 1];
-    if (pr.flags & MARLNAV_NOISY_AGENTS) {
+    if (NOISY) {
         const uint32_t base = (uint32_t)(2 * S);
         for (int i = 0; i < A; ++i) {
             const float u1 = native_uniform(pr.seed, gid, sidx, base + 3 * i);
@@ -308,21 +307,10 @@ __device__ __forceinline__ void stage_spans(Span a, Span b, Span c, int lane)
 {
     const bool vec = ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(b.src) |
                        reinterpret_cast<uintptr_t>(c.src)) & 15u) == 0;
-    if (!vec) {  // unaligned tile base (tiny W): scalar loads, all in flight
-        float r0[4 * KMAX];
+    if (!vec) {  // unaligned tile base (only W < 4 tiles): plain copy
         const int nt = a.n + b.n + c.n;
-#pragma unroll
-        for (int k = 0; k < 4 * KMAX; ++k) {
-            const int i = lane + 64 * k;
-            if (i < nt) r0[k] = *span_src(a, b, c, i, a.n, b.n);
-        }
-        for (int i = lane + 64 * 4 * KMAX; i < nt; i += 64)
+        for (int i = lane; i < nt; i += 64)
             *span_dst(a, b, c, i, a.n, b.n) = *span_src(a, b, c, i, a.n, b.n);
-#pragma unroll
-        for (int k = 0; k < 4 * KMAX; ++k) {
-            const int i = lane + 64 * k;
-            if (i < nt) *span_dst(a, b, c, i, a.n, b.n) = r0[k];
-        }
         return;
     }
     const int va = a.n >> 2, vb = b.n >> 2, vc = c.n >> 2;
@@ -516,7 +504,7 @@ struct StepArgs {
 };
 
 // --------------------------------------------------------------- step kernel
-template <int A_T, int O_T, bool OBS_ONLY>
+template <int A_T, int O_T, bool OBS_ONLY, bool NOISY = false>
 __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args, MarlnavParams pr)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -541,11 +529,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
     const bool norm = !OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM) != 0;
     const int el = lane / A, a = lane - el * A;
     unsigned c_trunc = 0, c_col = 0, c_tar = 0;
-#if MARLNAV_STAMPS
-    bool first = true;
-#endif
 
-    for (int64_t tile = gw; tile < args.ntiles; tile += args.waves) {
+    // one tile per wave (a grid-stride loop here makes the compiler keep every
+    // loop-invariant parameter live in registers: 160+ VGPRs instead of ~80)
+    {
+        const int64_t tile = gw;
+        if (tile >= args.ntiles) return;
         STAMP(0);
         const int64_t e0 = tile * W;
         const int ne = (int)((args.P - e0) < W ? (args.P - e0) : W);
@@ -610,7 +599,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
 
         if (!OBS_ONLY) {
             // ---- per-env reductions, terminal logic, masked re-init
-            bool fin = false;
+            bool fin = false, tr_l = false, co_l = false, ta_l = false;
             if (env_on) {
                 const int64_t e = e0 + lane;
                 unsigned any_col = 0u, all_in = 1u;
@@ -630,9 +619,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                 b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
                 b.terminated[e] = (uint8_t)terminated;
                 b.truncated[e] = (uint8_t)truncated;
-                c_trunc += truncated;
-                c_col += any_col;
-                c_tar += all_in;
                 fin = truncated || terminated;                     // :102-104
                 if (fin) {
                     float *sts = st + 5 * A * lane;
@@ -645,8 +631,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                         tge[0] = b.fresh_target[2 * e];
                         tge[1] = b.fresh_target[2 * e + 1];
                     } else {
-                        native_fresh_env(A, S, pr, b.formation, (uint64_t)(args.env_offset + e),
-                                         args.step_idx, sts, obe, tge);
+                        native_fresh_env<NOISY>(A, S, pr, b.formation,
+                                                (uint64_t)(args.env_offset + e), args.step_idx,
+                                                sts, obe, tge);
                     }
                     for (int i = 0; i < 2 * S; ++i) b.obstacles[e * S * 2 + i] = obe[i];
                     b.target[2 * e] = tge[0];
@@ -655,7 +642,13 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                 }
                 b.step_num[e] = step_num;
                 envbits[lane] = fin ? 1u : 0u;
+                tr_l = truncated;
+                co_l = any_col;
+                ta_l = all_in;
             }
+            c_trunc += __popcll(__ballot(tr_l));
+            c_col += __popcll(__ballot(co_l));
+            c_tar += __popcll(__ballot(ta_l));
             const bool any_fin = __ballot(fin) != 0ull;
             wave_sync();
             STAMP(4);
@@ -681,12 +674,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
         if (!OBS_ONLY)
             wave_store(b.states + e0 * A * 5, st, nr * 5, lane, nullptr, nullptr, nullptr, 1);
         STAMP(6);
-#if MARLNAV_STAMPS
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        STAMP(7);
-        first = false;
-#endif
-        wave_sync();  // the next tile overwrites this slice
     }
     if (!OBS_ONLY && b.counters && lane == 0) {
         // this wave's own slots: contention-free, fire-and-forget
@@ -694,6 +681,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
         if (c_col) atomicAdd(&b.counters[1 * args.waves + gw], (unsigned long long)c_col);
         if (c_tar) atomicAdd(&b.counters[2 * args.waves + gw], (unsigned long long)c_tar);
     }
+#if MARLNAV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(7);
+#endif
 }
 
 // ----------------------------------------------------- native reinit kernel
@@ -703,8 +694,12 @@ __global__ void reinit_all_kernel(int64_t P, int A, int S, int64_t env_offset, u
 {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= P) return;
-    native_fresh_env(A, S, pr, formation, (uint64_t)(env_offset + e), sidx, states + e * A * 5,
-                     obstacles + e * S * 2, target + 2 * e);
+    if (pr.flags & MARLNAV_NOISY_AGENTS)
+        native_fresh_env<true>(A, S, pr, formation, (uint64_t)(env_offset + e), sidx,
+                               states + e * A * 5, obstacles + e * S * 2, target + 2 * e);
+    else
+        native_fresh_env<false>(A, S, pr, formation, (uint64_t)(env_offset + e), sidx,
+                                states + e * A * 5, obstacles + e * S * 2, target + 2 * e);
 }
 
 __global__ void counters_total_kernel(const uint64_t *__restrict__ c, int64_t slots,
@@ -742,8 +737,7 @@ Launch plan_launch(const MarlnavDims *d)
     L.W = pick_wave_envs(d->num_agents, d->num_obstacles, d->obstacle_stride);
     L.plan = make_plan(L.W, d->num_agents, d->num_obstacles, d->obstacle_stride);
     L.ntiles = (d->num_parallel + L.W - 1) / L.W;
-    L.waves = L.ntiles < kMaxWaves ? L.ntiles : kMaxWaves;
-    L.waves = (L.waves + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+    L.waves = (L.ntiles + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
     L.blocks = L.waves / kWavesPerBlock;
     return L;
 }
@@ -771,22 +765,24 @@ using StepFn = void (*)(StepArgs, MarlnavParams);
 
 struct KernelPair {
     int A, O;
-    StepFn step, obs;
+    StepFn step, obs, noisy;
 };
 
 const KernelPair kVariants[] = {
-    {3, 3, wave_kernel<3, 3, false>, wave_kernel<3, 3, true>},
-    {3, 8, wave_kernel<3, 8, false>, wave_kernel<3, 8, true>},
-    {3, 1, wave_kernel<3, 1, false>, wave_kernel<3, 1, true>},
-    {2, 1, wave_kernel<2, 1, false>, wave_kernel<2, 1, true>},
-    {16, 32, wave_kernel<16, 32, false>, wave_kernel<16, 32, true>},
+    {3, 3, wave_kernel<3, 3, false>, wave_kernel<3, 3, true>, wave_kernel<3, 3, false, true>},
+    {3, 8, wave_kernel<3, 8, false>, wave_kernel<3, 8, true>, wave_kernel<3, 8, false, true>},
+    {3, 1, wave_kernel<3, 1, false>, wave_kernel<3, 1, true>, wave_kernel<3, 1, false, true>},
+    {2, 1, wave_kernel<2, 1, false>, wave_kernel<2, 1, true>, wave_kernel<2, 1, false, true>},
+    {16, 32, wave_kernel<16, 32, false>, wave_kernel<16, 32, true>,
+     wave_kernel<16, 32, false, true>},
 };
 
 KernelPair select_kernels(int A, int O)
 {
     for (const KernelPair &k : kVariants)
         if (k.A == A && k.O == O) return k;
-    return KernelPair{0, 0, wave_kernel<0, 0, false>, wave_kernel<0, 0, true>};
+    return KernelPair{0, 0, wave_kernel<0, 0, false>, wave_kernel<0, 0, true>,
+                      wave_kernel<0, 0, false, true>};
 }
 
 StepArgs make_args(const MarlnavDims *d, const Launch &L)
@@ -858,8 +854,9 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavSte
     StepArgs args = make_args(d, L);
     args.b = *b;
     args.step_idx = step_idx;
-    return launch(select_kernels(d->num_agents, d->num_obstacles).step, L, args, *pr, stream,
-                  "marlnav_step");
+    const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
+    const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
+    return launch(noisy ? k.noisy : k.step, L, args, *pr, stream, "marlnav_step");
 }
 
 int marlnav_observe(const MarlnavDims *d, const float *states, const float *obstacles,

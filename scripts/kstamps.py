@@ -37,6 +37,7 @@ def main():
             env.step(acts)
             torch.cuda.synchronize()
             st = buf.view(nb, 8, 2).cpu().numpy().astype(np.int64)
+            st = st[st[:, 0, 0] > 0]  # waves past the last tile record nothing
             rt = st[:, :, 0] * 10.0 / 1e3  # 100 MHz ticks -> us
             cy = st[:, :, 1]
             t0 = rt[:, 0].min()
