@@ -103,6 +103,33 @@ __device__ __forceinline__ float pair_dist(float ox, float oy, float px, float p
 #endif
 }
 
+// Two correctly rounded quotients over one denominator. This is hipcc's
+// own IEEE fp32 division sequence (reciprocal refined by one Newton step,
+// two residual corrections) with the v_div_scale / v_div_fixup range steps
+// dropped and the reciprocal shared, valid when no operand or quotient needs
+// rescaling: den in [2^-64, 2^64] and each numerator 0 or in [2^-64, 2^64]
+// (there both steps are the identity). Outside that range, plain division.
+// Verified bit-exact against IEEE division: scripts/probes/div_probe.hip.
+__device__ __forceinline__ void div2(float x, float y, float den, float *qx, float *qy)
+{
+    const float ax = fabsf(x), ay = fabsf(y), ad = fabsf(den);
+    const bool fast = ad >= 0x1p-64f && ad <= 0x1p64f && (x == 0.0f || (ax >= 0x1p-64f && ax <= 0x1p64f)) &&
+                      (y == 0.0f || (ay >= 0x1p-64f && ay <= 0x1p64f));
+    if (__builtin_expect(fast, 1)) {
+        float r = __builtin_amdgcn_rcpf(den);
+        r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+        float q = x * r;
+        q = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
+        *qx = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
+        q = y * r;
+        q = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
+        *qy = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
+    } else {
+        *qx = x / den;
+        *qy = y / den;
+    }
+}
+
 // _get_angles (environment.py:276-286) + the dist < 0.1 cap (:172-177)
 __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float py,
                                             float dirx, float diry, float dist, float cap)
@@ -112,7 +139,8 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
 #if MARLNAV_ABLATE & 4
     const float nx = __fdividef(dx, den), ny = __fdividef(dy, den);
 #else
-    const float nx = dx / den, ny = dy / den;
+    float nx, ny;
+    div2(dx, dy, den, &nx, &ny);
 #endif
     float dot = dirx * nx + diry * ny;
     dot = clamp_t(dot, -1.0f, 1.0f);
