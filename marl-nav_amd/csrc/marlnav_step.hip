@@ -60,7 +60,7 @@ __device__ unsigned long long *g_stamps;
 #define STAMP(k)                                                                   \
     do {                                                                           \
         if (lane == 0) {                                                           \
-            unsigned long long *sp_ = g_stamps + (size_t)gw * 16;                  \
+            unsigned long long *sp_ = g_stamps + (size_t)gw * 24;                  \
             sp_[2 * (k)] = wall_clock64();                                         \
             sp_[2 * (k) + 1] = clock64();                                          \
         }                                                                          \
@@ -103,19 +103,18 @@ __device__ __forceinline__ float pair_dist(float ox, float oy, float px, float p
 #endif
 }
 
-// Two correctly rounded quotients over one denominator. This is hipcc's
-// own IEEE fp32 division sequence (reciprocal refined by one Newton step,
-// two residual corrections) with the v_div_scale / v_div_fixup range steps
-// dropped and the reciprocal shared, valid when no operand or quotient needs
-// rescaling: den in [2^-64, 2^64] and each numerator 0 or in [2^-64, 2^64]
-// (there both steps are the identity). Outside that range, plain division.
-// Verified bit-exact against IEEE division: scripts/probes/div_probe.hip.
+// Two correctly rounded quotients over one denominator. This is hipcc's own
+// IEEE fp32 division sequence (reciprocal refined by one Newton step, two
+// residual corrections) with the v_div_scale / v_div_fixup range steps
+// dropped and the reciprocal shared. The caller guarantees den >= 1e-12 and
+// |x|, |y| <= ~den (den is the pair distance), so quotients lie in [-1, 1]
+// and, for den <= 2^96, no operand needs the range steps. Larger or non-finite
+// den takes plain division. Verified bit-exact against IEEE division on the
+// GPU over this domain, denormal numerators included:
+// scripts/probes/div_probe.hip.
 __device__ __forceinline__ void div2(float x, float y, float den, float *qx, float *qy)
 {
-    const float ax = fabsf(x), ay = fabsf(y), ad = fabsf(den);
-    const bool fast = ad >= 0x1p-64f && ad <= 0x1p64f && (x == 0.0f || (ax >= 0x1p-64f && ax <= 0x1p64f)) &&
-                      (y == 0.0f || (ay >= 0x1p-64f && ay <= 0x1p64f));
-    if (__builtin_expect(fast, 1)) {
+    if (__builtin_expect(den <= 0x1p96f, 1)) {
         float r = __builtin_amdgcn_rcpf(den);
         r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
         float q = x * r;
@@ -714,6 +713,10 @@ template <int A_T, int O_T, bool OBS_ONLY, bool NOISY = false>
 __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args, MarlnavParams pr)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+#if MARLNAV_STAMPS
+    unsigned long long t_entry;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
+#endif
     const int A = A_T ? A_T : args.A;
     const int O = O_T ? O_T : args.O;
     const int S = args.S, W = args.W;
@@ -921,6 +924,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
 #if MARLNAV_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     STAMP(7);
+    if (lane == 0) g_stamps[(size_t)gw * 24 + 16] = t_entry;
 #endif
 }
 

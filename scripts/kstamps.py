@@ -25,7 +25,7 @@ def main():
         lib = env._lib
         lib.marlnav_debug_stamps.argtypes = [ctypes.c_void_p]
         nb = env._counters.shape[1]
-        buf = torch.zeros(nb * 16, dtype=torch.int64, device="cuda")
+        buf = torch.zeros(nb * 24, dtype=torch.int64, device="cuda")
         assert lib.marlnav_debug_stamps(buf.data_ptr()) == 0
         acts = torch.zeros(P, A, 2, device="cuda")
         acts[..., 0] = 0.1
@@ -36,16 +36,20 @@ def main():
         for _ in range(5):
             env.step(acts)
             torch.cuda.synchronize()
-            st = buf.view(nb, 8, 2).cpu().numpy().astype(np.int64)
-            st = st[st[:, 0, 0] > 0]  # waves past the last tile record nothing
+            raw = buf.view(nb, 24).cpu().numpy().astype(np.int64)
+            raw = raw[raw[:, 0] > 0]  # waves past the last tile record nothing
+            st = raw[:, :16].reshape(-1, 8, 2)
+            entry = raw[:, 16] * 10.0 / 1e3
             rt = st[:, :, 0] * 10.0 / 1e3  # 100 MHz ticks -> us
             cy = st[:, :, 1]
-            t0 = rt[:, 0].min()
+            t0 = entry.min()
             ph = np.diff(rt, axis=1)
             clk = (cy[:, 7] - cy[:, 0]) / np.maximum(rt[:, 7] - rt[:, 0], 1e-3) / 1e3
             res.append({
                 "span_us": round(float(rt[:, 7].max() - t0), 2),
-                "start_spread_us": round(float(rt[:, 0].max() - t0), 2),
+                "entry_spread_us": round(float(entry.max() - t0), 2),
+                "entry_to_t0_median_us": round(float(np.median(rt[:, 0] - entry)), 2),
+                "entry_to_t0_p90_us": round(float(np.percentile(rt[:, 0] - entry, 90)), 2),
                 "last_stored_us": round(float(rt[:, 6].max() - t0), 2),
                 "phase_median_us": {n: round(float(np.median(ph[:, i])), 3)
                                     for i, n in enumerate(names)},

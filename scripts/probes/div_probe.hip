@@ -9,6 +9,7 @@
 
 __device__ __forceinline__ void div2(float x, float y, float den, float *qx, float *qy)
 {
+    if (!(den <= 0x1p96f)) { *qx = x / den; *qy = y / den; return; }
     float r = __builtin_amdgcn_rcpf(den);
     r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
     float q = x * r;
@@ -32,18 +33,23 @@ __global__ void probe(uint64_t seed, uint64_t n, unsigned long long *bad, float 
         const uint32_t h1 = hash(seed * 0x9E3779B97F4A7C15ull + 3 * i);
         const uint32_t h2 = hash(seed * 0x9E3779B97F4A7C15ull + 3 * i + 1);
         const uint32_t h3 = hash(seed * 0x9E3779B97F4A7C15ull + 3 * i + 2);
-        float x, y, d;
-        if (i & 1) {  // kernel-like: differences of positions, distances
-            x = ((float)(h1 >> 8) * 0x1p-24f - 0.5f) * 4000.0f;
-            y = ((float)(h2 >> 8) * 0x1p-24f - 0.5f) * 4000.0f;
-            d = __builtin_sqrtf(__builtin_fmaf(y, y, x * x));
-            if ((h3 & 7) == 0) d = 1e-12f;
-            if ((h3 & 15) == 1) { x *= 1e-6f; y *= 1e-6f; d = __builtin_sqrtf(__builtin_fmaf(y, y, x * x)); }
-        } else {      // random bit patterns with exponents in [-64, 64]
-            x = __uint_as_float((h1 & 0x807FFFFFu) | ((uint32_t)(63 + (h1 >> 24) % 129) << 23));
-            y = __uint_as_float((h2 & 0x807FFFFFu) | ((uint32_t)(63 + (h2 >> 24) % 129) << 23));
-            d = __uint_as_float((h3 & 0x007FFFFFu) | ((uint32_t)(63 + (h3 >> 24) % 129) << 23));
+        // the kernel's domain: den = max(sqrt(fma(y, y, x*x)), 1e-12), so |x|, |y| <~ den
+        const int mode = (int)(i % 4);
+        const float ux = (float)(h1 >> 8) * 0x1p-24f - 0.5f, uy = (float)(h2 >> 8) * 0x1p-24f - 0.5f;
+        float x, y;
+        if (mode == 0) {        // positions up to 1e4 apart
+            x = ux * 4000.0f; y = uy * 4000.0f;
+        } else if (mode == 1) { // random exponents down to denormals
+            const float sx = __uint_as_float(((uint32_t)(h3 % 254) << 23) | (h1 & 0x807FFFFFu));
+            x = sx; y = uy * sx * 2.0f;
+        } else if (mode == 2) { // tiny differences (clamped denominators)
+            x = ux * 1e-11f; y = uy * 1e-11f;
+        } else {                // huge magnitudes up to 2^96
+            const float sc = __uint_as_float(((uint32_t)(127 + h3 % 97) << 23));
+            x = ux * sc; y = uy * sc;
         }
+        float d = __builtin_sqrtf(__builtin_fmaf(y, y, x * x));
+        d = d > 1e-12f ? d : 1e-12f;
         float qx, qy;
         div2(x, y, d, &qx, &qy);
         const float rx = x / d, ry = y / d;
@@ -67,7 +73,7 @@ int main()
     float e[12] = {0};
     hipMemcpy(&h, bad, 8, hipMemcpyDeviceToHost);
     hipMemcpy(e, ex, 48, hipMemcpyDeviceToHost);
-    printf("div2 vs IEEE: %llu mismatches in %llu quotient pairs\n", h, 4ull * n);
+    printf("div2 vs IEEE (kernel domain): %llu mismatches in %llu quotient pairs\n", h, 4ull * n);
     for (int k = 0; k < 4 && k < (int)h; ++k) printf("  x=%a y=%a d=%a\n", e[3 * k], e[3 * k + 1], e[3 * k + 2]);
     return h != 0;
 }
