@@ -108,13 +108,16 @@ __device__ __forceinline__ float pair_dist(float ox, float oy, float px, float p
 // residual corrections) with the v_div_scale / v_div_fixup range steps
 // dropped and the reciprocal shared. The caller guarantees den >= 1e-12 and
 // |x|, |y| <= ~den (den is the pair distance), so quotients lie in [-1, 1]
-// and, for den <= 2^96, no operand needs the range steps. Larger or non-finite
-// den takes plain division. Verified bit-exact against IEEE division on the
+// and, for den <= 2^96 and normal-or-zero numerators, no operand needs the
+// range steps. Other inputs (huge or non-finite den, denormal numerators)
+// take plain division. Verified bit-exact against IEEE division on the
 // GPU over this domain, denormal numerators included:
 // scripts/probes/div_probe.hip.
 __device__ __forceinline__ void div2(float x, float y, float den, float *qx, float *qy)
 {
-    if (__builtin_expect(den <= 0x1p96f, 1)) {
+    // 0x90: +-denormal; a denormal numerator needs the range steps
+    const bool sub = __builtin_amdgcn_classf(x, 0x90) | __builtin_amdgcn_classf(y, 0x90);
+    if (__builtin_expect(den <= 0x1p96f && !sub, 1)) {
         float r = __builtin_amdgcn_rcpf(den);
         r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
         float q = x * r;
@@ -742,6 +745,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
     const int el = lane / A, a = lane - el * A;
     unsigned c_trunc = 0, c_col = 0, c_tar = 0;
 
+#if MARLNAV_STAMPS && (MARLNAV_ABLATE & 32)
+    if ((threadIdx.x & 63) == 0) {  // dispatch-only probe: entry stamp and out
+        const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+        for (int k = 0; k < 16; ++k) g_stamps[w * 24 + k] = t_entry;
+        g_stamps[w * 24 + 16] = t_entry;
+        g_stamps[w * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+    }
+    return;
+#endif
     // one tile per wave (a grid-stride loop here makes the compiler keep every
     // loop-invariant parameter live in registers: 160+ VGPRs instead of ~80)
     {
@@ -924,7 +936,11 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
 #if MARLNAV_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     STAMP(7);
-    if (lane == 0) g_stamps[(size_t)gw * 24 + 16] = t_entry;
+    if (lane == 0) {
+        g_stamps[(size_t)gw * 24 + 16] = t_entry;
+        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+    }
 #endif
 }
 

@@ -7,7 +7,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["MARLNAV_LIB"] = os.path.join(ROOT, "marl-nav_amd", "lib", "stamps.so")
+os.environ["MARLNAV_LIB"] = os.path.join(ROOT, "marl-nav_amd", "lib",
+                                         os.environ.get("STAMPS_LIB", "stamps.so"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -58,6 +59,14 @@ def main():
                 "block_total_median_us": round(float(np.median(rt[:, 7] - rt[:, 0])), 2),
                 "clock_ghz_median": round(float(np.median(clk)), 2)})
         print(cfg, json.dumps(res[-1]))
+        # entry time by XCC (dispatch placement)
+        xcc = raw[:, 18] & 0xF
+        e_rel = entry - entry.min()
+        print(cfg, "entry_us by xcc (median, max):",
+              {int(x): (round(float(np.median(e_rel[xcc == x])), 2),
+                        round(float(e_rel[xcc == x].max()), 2)) for x in np.unique(xcc)})
+        print(cfg, "entry percentiles us:", [round(float(np.percentile(e_rel, q)), 2)
+                                             for q in (0, 10, 25, 50, 75, 90, 100)])
         print(cfg, "spans", [r["span_us"] for r in res])
         del env
 

@@ -9,7 +9,8 @@
 
 __device__ __forceinline__ void div2(float x, float y, float den, float *qx, float *qy)
 {
-    if (!(den <= 0x1p96f)) { *qx = x / den; *qy = y / den; return; }
+    const bool sub = __builtin_amdgcn_classf(x, 0x90) | __builtin_amdgcn_classf(y, 0x90);
+    if (!(den <= 0x1p96f) || sub) { *qx = x / den; *qy = y / den; return; }
     float r = __builtin_amdgcn_rcpf(den);
     r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
     float q = x * r;
