@@ -16,8 +16,8 @@ Timing: W untimed steps; barrier + synchronize; K timed steps; synchronize +
 barrier; the max over ranks. value = N*P*K / max time.
 
 roofline: the step kernel's average duration from HIP events recorded on the
-launch stream around each launch of a second, GPU-saturated pass (a device
-sleep gives the host a head start so no launch waits on Python), against the
+launch stream around replays of a hipGraph of back-to-back Env.step launches
+(so no kernel waits on Python; the graph's inter-kernel gap is included), against the
 algorithmic bytes per env-step (read 28A+8O+13, write 20A+4A*D+11: 336 B at
 A3/O3) and the 8 TB/s HBM peak. traffic: HBM bytes per launch from the
 committed rocprofv3 PMC summary for this config (profiles/), or null.
@@ -53,7 +53,6 @@ def parse():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--agents", type=int, default=3)
     ap.add_argument("--obstacles", type=int, default=3)
-    ap.add_argument("--kernel-steps", type=int, default=200)
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -81,20 +80,35 @@ def make_actions(P, A, device, rank, n=64):
     return out
 
 
-def kernel_time_us(env, actions, n):
-    """Average step-kernel duration from per-launch HIP events on the launch
-    stream, with the GPU kept ahead of the host by a device-side sleep."""
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
-    stops = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+def kernel_time_us(env, actions, n=25, replays=12):
+    """Average step-kernel time from HIP events on the launch stream around
+    replays of a hipGraph holding n back-to-back Env.step launches (no host
+    gaps between kernels; each interval includes the graph's inter-kernel
+    boundary, so this slightly overstates the kernel duration)."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for i in range(3):
+            env.step(actions[i % len(actions)])
+    torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
-    torch.cuda._sleep(int(60e6))  # ~25-40 ms head start at 1.5-2.4 GHz
-    for i in range(n):
-        starts[i].record()
-        env.step(actions[i % len(actions)])
-        stops[i].record()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for i in range(n):
+            env.step(actions[i % len(actions)])
+    graph.replay()
     torch.cuda.synchronize()
-    t = sorted(s.elapsed_time(e) * 1e3 for s, e in zip(starts, stops))
-    return sum(t) / n, t[len(t) // 2]
+    per = []
+    for _ in range(replays):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        graph.replay()
+        e.record()
+        e.synchronize()
+        per.append(s.elapsed_time(e) * 1e3 / n)
+    per.sort()
+    return sum(per) / len(per), per[len(per) // 2]
 
 
 def cpu_baseline(P, A, O, seconds, threads):
@@ -170,7 +184,7 @@ def main():
     dt = time.perf_counter() - t0
     dt = pkg.shard.max_over_ranks(dt, device)
 
-    kern_avg, kern_med = kernel_time_us(env, actions, a.kernel_steps)
+    kern_avg, kern_med = kernel_time_us(env, actions)
     per_env = alg_bytes_per_env(A, O)
     launch_bytes = per_env * P
     achieved = launch_bytes / (kern_avg * 1e-6) / 1e9

@@ -92,7 +92,9 @@ def make_cparams(values, init=None, seed=0, flags=0):
 
 
 def _stream_handle(device):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """Raw handle of the current HIP stream of `device` (the stream torch
+    launches on; a capture stream under torch.cuda.graph)."""
+    return torch._C._cuda_getCurrentRawStream(device.index)
 
 
 class Env(object):
@@ -158,6 +160,9 @@ class Env(object):
         self._dims = abi.MarlnavDims()
         self._cparams = abi.MarlnavParams()
         self._bufs = abi.MarlnavStepBuffers()
+        self._dims_ref = ctypes.byref(self._dims)
+        self._cparams_ref = ctypes.byref(self._cparams)
+        self._bufs_ref = ctypes.byref(self._bufs)
         self._formation = None
         if is_triangle:
             smp = self._init_sampler
@@ -241,6 +246,8 @@ class Env(object):
         d.reserved = 0
         d.env_offset = self._env_offset
         self._obs_dim = 2 + 2 * d.num_obstacles + 2 * (self.num_agents - 1)
+        self._obs_shape = (self.num_parallel, self.num_agents, self._obs_dim)
+        self._act_shape = (self.num_parallel, self.num_agents, 2)
         O = d.num_obstacles
         self._split = [1, 1, O, O, self.num_agents - 1, self.num_agents - 1]
         if hasattr(self, '_counters') and old != (d.num_agents, d.num_obstacles, S):
@@ -256,6 +263,7 @@ class Env(object):
         init = self._default_init_sampler if self._formation is not None else None
         self._cparams = make_cparams(values, init=init, seed=self._seed,
                                      flags=self._cparams.flags)
+        self._cparams_ref = ctypes.byref(self._cparams)
         object.__setattr__(self, '_params_dirty', False)
 
     def _new_obs(self):
@@ -263,8 +271,11 @@ class Env(object):
                            dtype=_F32, device=self.device)
 
     def _wrap_obs(self, packed, normalized=None):
-        obs = Observations(*torch.split(packed, self._split, dim=2))
-        return _PackedObservations(obs, packed, normalized, self._normalizer)
+        o = tuple.__new__(_PackedObservations, torch.split(packed, self._split, 2))
+        o._packed = packed
+        o._normalized = normalized
+        o._normalizer = self._normalizer
+        return o
 
     # ------------------------------------------------------------ state API
     @property
@@ -392,22 +403,27 @@ class Env(object):
             self._target.data_ptr(), out.data_ptr(), _stream_handle(self.device)), self._lib)
         return self._wrap_obs(out)
 
+    def _coerce_actions(self, actions):
+        actions = torch.as_tensor(actions)
+        if actions.shape[-1] != 2:
+            actions = actions[..., [0, -1]]  # angle = [..., 0], accel = [..., -1]
+        actions = actions.to(device=self.device, dtype=_F32).contiguous()
+        if tuple(actions.shape) != self._act_shape:
+            raise ValueError(f"actions must be {self._act_shape}, got {tuple(actions.shape)}")
+        return actions
+
     def step(self, actions):
         """environment.py:92-107: returns (Observations, rewards (P,),
         terminated (P,) bool, truncated (P,) bool)."""
-        self._sync_params()
-        P, dev = self.num_parallel, self.device
-        if not (isinstance(actions, torch.Tensor) and actions.device == dev
-                and actions.dtype == _F32 and actions.shape[-1] == 2
+        if self._params_dirty:
+            self._sync_params()
+        dev = self.device
+        if not (type(actions) is torch.Tensor and actions.dtype is _F32
+                and actions.device == dev and actions.shape == self._act_shape
                 and actions.is_contiguous()):
-            actions = torch.as_tensor(actions)
-            if actions.shape[-1] != 2:
-                actions = actions[..., [0, -1]]  # angle = [..., 0], accel = [..., -1]
-            actions = actions.to(device=dev, dtype=_F32).contiguous()
-        if tuple(actions.shape) != (P, self.num_agents, 2):
-            raise ValueError(f"actions must be ({P}, {self.num_agents}, 2), "
-                             f"got {tuple(actions.shape)}")
-        obs = self._new_obs()
+            actions = self._coerce_actions(actions)
+        P = self.num_parallel
+        obs = torch.empty(self._obs_shape, dtype=_F32, device=dev)
         reward = torch.empty(P, dtype=_F32, device=dev)
         terminated = torch.empty(P, dtype=torch.bool, device=dev)
         truncated = torch.empty(P, dtype=torch.bool, device=dev)
@@ -415,15 +431,16 @@ class Env(object):
         b.states = self._states.data_ptr()
         b.obstacles = self._obstacles.data_ptr()
         b.target = self._target.data_ptr()
-        b.step_num = self._step_num.data_ptr()
-        b.terminates = self._terminates.data_ptr()
+        b.step_num = self.__dict__['_step_num_t'].data_ptr()
+        b.terminates = self.__dict__['_terminates_t'].data_ptr()
         b.actions = actions.data_ptr()
         b.obs = obs.data_ptr()
         b.reward = reward.data_ptr()
         b.terminated = terminated.data_ptr()
         b.truncated = truncated.data_ptr()
         b.counters = self._counters.data_ptr()
-        flags = self._cparams.flags & ~(abi.FRESH_STATES_FROM_MOVED | abi.WRITE_OBS_NORM)
+        cp = self._cparams
+        flags = cp.flags & ~(abi.FRESH_STATES_FROM_MOVED | abi.WRITE_OBS_NORM)
         keep = None
         if self._rng == 'native' and self._init_sampler is self._default_init_sampler:
             b.fresh_states = b.fresh_obstacles = b.fresh_target = None
@@ -439,25 +456,27 @@ class Env(object):
                 flags |= abi.FRESH_STATES_FROM_MOVED
         normalized = None
         if self._obs_norm_buffers is not None:
-            normalized = self._new_obs()
+            normalized = torch.empty(self._obs_shape, dtype=_F32, device=dev)
             b.obs_norm = normalized.data_ptr()
             b.norm_mean = self._obs_norm_buffers[0].data_ptr()
             b.norm_scale = self._obs_norm_buffers[1].data_ptr()
             flags |= abi.WRITE_OBS_NORM
-        self._cparams.flags = flags
-        abi.check(self._lib.marlnav_step(
-            ctypes.byref(self._dims), ctypes.byref(self._cparams), ctypes.byref(b),
-            self._step_idx, _stream_handle(dev)), self._lib)
-        self._step_idx += 1
+        cp.flags = flags
+        d = self.__dict__
+        rc = self._lib.marlnav_step(self._dims_ref, self._cparams_ref, self._bufs_ref,
+                                    d['_step_idx'], _stream_handle(dev))
+        if rc:
+            abi.check(rc, self._lib)
+        d['_step_idx'] += 1
         if self._mock_alias:
             # the reference's MockInitializer now holds the post-move states
             # (utils.py:310-319 aliasing); later re-inits restore them
-            self._mock_alias = False
+            d['_mock_alias'] = False
             init = self._init_sampler
             if isinstance(init, MockInitializer):
                 init.states = self._states.clone()
-        self._last_finished = (terminated, truncated)
-        self.__dict__['_reinit_mask_t'] = None
+        d['_last_finished'] = (terminated, truncated)
+        d['_reinit_mask_t'] = None
         del keep
         return self._wrap_obs(obs, normalized), reward, terminated, truncated
 
@@ -465,11 +484,5 @@ class Env(object):
 class _PackedObservations(Observations):
     """``Observations`` whose six fields are views of one packed (P, A, D)
     tensor (the layout of ObsNormalizer's torch.cat, utils.py:531); carries
-    that tensor and, when a normalizer is attached, the kernel-normalized one."""
-
-    def __new__(cls, obs, packed, normalized, normalizer):
-        self = super().__new__(cls, *obs)
-        self._packed = packed
-        self._normalized = normalized
-        self._normalizer = normalizer
-        return self
+    that tensor and, when a normalizer is attached, the kernel-normalized one
+    (set by Env._wrap_obs)."""

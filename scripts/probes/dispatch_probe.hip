@@ -15,7 +15,7 @@ __global__ void probe(unsigned long long *t, int nwaves_per_block, Big big)
     if ((threadIdx.x & 63) == 0) {
         const int w = blockIdx.x * nwaves_per_block + (threadIdx.x >> 6);
         t[2 * w] = now;
-        t[2 * w + 1] = wall_clock64();
+        t[2 * w + 1] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
     }
     if (big.f[0] == 12345.0f) lds[threadIdx.x] = big.f[threadIdx.x % 40];
 }
@@ -48,11 +48,22 @@ int main()
             std::vector<unsigned long long> h(2 * blocks * wpb);
             hipMemcpy(h.data(), t, h.size() * 8, hipMemcpyDeviceToHost);
             unsigned long long lo = ~0ull, hi = 0;
+            unsigned long long xlo[16], xhi[16];
+            for (int x = 0; x < 16; ++x) { xlo[x] = ~0ull; xhi[x] = 0; }
             for (int w = 0; w < blocks * wpb; ++w) {
                 lo = std::min(lo, h[2 * w]);
                 hi = std::max(hi, h[2 * w]);
+                const int x = (int)(h[2 * w + 1] & 15);
+                xlo[x] = std::min(xlo[x], h[2 * w]);
+                xhi[x] = std::max(xhi[x], h[2 * w]);
             }
             spread.push_back((hi - lo) * 0.01);  // 100 MHz -> us
+            if (rep == 19) {
+                printf("   per-xcc first/last entry (us):");
+                for (int x = 0; x < 16; ++x)
+                    if (xhi[x]) printf(" %d:%.2f/%.2f", x, (xlo[x] - lo) * 0.01, (xhi[x] - lo) * 0.01);
+                printf("\n");
+            }
         }
         std::sort(ms.begin(), ms.end());
         std::sort(spread.begin(), spread.end());
