@@ -34,8 +34,10 @@ def main():
             env.step(acts)
         torch.cuda.synchronize()
         res = []
+        b2b = int(os.environ.get("B2B", "1"))
         for _ in range(5):
-            env.step(acts)
+            for _ in range(b2b):  # back-to-back launches: keep every XCD busy
+                env.step(acts)
             torch.cuda.synchronize()
             raw = buf.view(nb, 24).cpu().numpy().astype(np.int64)
             raw = raw[raw[:, 0] > 0]  # waves past the last tile record nothing
