@@ -109,32 +109,31 @@ __device__ __forceinline__ float pair_dist(float ox, float oy, float px, float p
 // dropped and the reciprocal shared. The caller guarantees den >= 1e-12 and
 // |x|, |y| <= ~den (den is the pair distance), so quotients lie in [-1, 1]
 // and, for den <= 2^96 and normal-or-zero numerators, no operand needs the
-// range steps. Other inputs (huge or non-finite den, denormal numerators)
-// take plain division. Verified bit-exact against IEEE division on the
-// GPU over this domain, denormal numerators included:
-// scripts/probes/div_probe.hip.
-__device__ __forceinline__ void div2(float x, float y, float den, float *qx, float *qy)
+// range steps; `ok` is cleared otherwise (huge or non-finite den, subnormal
+// numerators) and the caller redoes the row with IEEE division. Branch-free,
+// so consecutive pairs interleave. Verified bit-exact against IEEE division
+// on the GPU over this domain: scripts/probes/div_probe.hip.
+__device__ __forceinline__ void div2_fast(float x, float y, float den, float *qx, float *qy,
+                                          bool &ok)
 {
-    // 0x90: +-denormal; a denormal numerator needs the range steps
-    const bool sub = __builtin_amdgcn_classf(x, 0x90) | __builtin_amdgcn_classf(y, 0x90);
-    if (__builtin_expect(den <= 0x1p96f && !sub, 1)) {
-        float r = __builtin_amdgcn_rcpf(den);
-        r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
-        float q = x * r;
-        q = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
-        *qx = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
-        q = y * r;
-        q = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
-        *qy = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
-    } else {
-        *qx = x / den;
-        *qy = y / den;
-    }
+    // 0x90: +-subnormal
+    ok &= (den <= 0x1p96f) & !__builtin_amdgcn_classf(x, 0x90) & !__builtin_amdgcn_classf(y, 0x90);
+    float r = __builtin_amdgcn_rcpf(den);
+    r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    float q = x * r;
+    q = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
+    *qx = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
+    q = y * r;
+    q = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
+    *qy = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
 }
 
-// _get_angles (environment.py:276-286) + the dist < 0.1 cap (:172-177)
+// _get_angles (environment.py:276-286) + the dist < 0.1 cap (:172-177).
+// FAST: shared-reciprocal division (clears ok when it may differ from IEEE).
+template <bool FAST = false>
 __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float py,
-                                            float dirx, float diry, float dist, float cap)
+                                            float dirx, float diry, float dist, float cap,
+                                            bool &ok)
 {
     const float dx = px - ox, dy = py - oy;
     const float den = dist > 1e-12f ? dist : 1e-12f;
@@ -142,7 +141,12 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
     const float nx = __fdividef(dx, den), ny = __fdividef(dy, den);
 #else
     float nx, ny;
-    div2(dx, dy, den, &nx, &ny);
+    if constexpr (FAST) {
+        div2_fast(dx, dy, den, &nx, &ny, ok);
+    } else {
+        nx = dx / den;
+        ny = dy / den;
+    }
 #endif
     float dot = dirx * nx + diry * ny;
     dot = clamp_t(dot, -1.0f, 1.0f);
@@ -224,11 +228,16 @@ __device__ void native_fresh_env(int A, int S, const MarlnavParams &pr,
                                  const float *__restrict__ formation, uint64_t gid,
                                  uint64_t sidx, float *st, float *ob, float *tg)
 {
-    for (int j = 0; j < S; ++j) {
-        const float ux = native_uniform(pr.seed, gid, sidx, (uint32_t)(2 * j));
-        const float uy = native_uniform(pr.seed, gid, sidx, (uint32_t)(2 * j + 1));
-        ob[2 * j] = pr.obs_range_x * (ux - 0.5f) + pr.obs_mean_x;
-        ob[2 * j + 1] = pr.obs_range_y * (uy - 0.5f) + pr.obs_mean_y;
+    for (int j = 0; j < S; j += 2) {  // one Philox block = 2 obstacles
+        uint32_t c[4] = {(uint32_t)(j >> 1), (uint32_t)sidx, (uint32_t)gid,
+                         (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
+        philox4x32_10(c, (uint32_t)pr.seed, (uint32_t)(pr.seed >> 32));
+        ob[2 * j] = pr.obs_range_x * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x;
+        ob[2 * j + 1] = pr.obs_range_y * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y;
+        if (j + 1 < S) {
+            ob[2 * j + 2] = pr.obs_range_x * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x;
+            ob[2 * j + 3] = pr.obs_range_y * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y;
+        }
     }
     for (int i = 0; i < 5 * A; ++i) st[i] = formation[i];
     tg[0] = formation[5 * A];
@@ -453,7 +462,8 @@ __device__ __forceinline__ RowOut observe_row(int Arun, int Orun, const float *_
 
     const float tx = tge[0], ty = tge[1];
     const float td = pair_dist(ox, oy, tx, ty);
-    const float ta = pair_angle(ox, oy, tx, ty, dx, dy, td, cap);
+    bool ok = true;
+    const float ta = pair_angle(ox, oy, tx, ty, dx, dy, td, cap, ok);
     row[0] = ta;
     row[1] = td;
 
@@ -462,7 +472,7 @@ __device__ __forceinline__ RowOut observe_row(int Arun, int Orun, const float *_
     for (int j = 0; j < O; ++j) {
         const float px = obe[2 * j], py = obe[2 * j + 1];
         const float d = pair_dist(ox, oy, px, py);
-        row[2 + j] = pair_angle(ox, oy, px, py, dx, dy, d, cap);
+        row[2 + j] = pair_angle(ox, oy, px, py, dx, dy, d, cap, ok);
         row[2 + O + j] = d;
         if (TERMS) {
             ob_risk |= d < pr.ob_risk_dist;
@@ -480,7 +490,7 @@ __device__ __forceinline__ RowOut observe_row(int Arun, int Orun, const float *_
         if (m == a) continue;
         const float px = sts[5 * m], py = sts[5 * m + 1];
         const float d = pair_dist(ox, oy, px, py);
-        ang_out[k] = pair_angle(ox, oy, px, py, dx, dy, d, cap);
+        ang_out[k] = pair_angle(ox, oy, px, py, dx, dy, d, cap, ok);
         dst_out[k] = d;
         ++k;
         if (TERMS) {
@@ -575,17 +585,18 @@ __device__ __forceinline__ float torch_row_sum_r(const float *x, F f)
 // observe_row with compile-time shape and the packed row kept in registers
 // (row[D]); others are visited as j = 0..A-2 -> agent j + (j >= a), so
 // every row index is a compile-time constant.
-template <int A, int O, bool TERMS>
+template <int A, int O, bool TERMS, bool FAST>
 __device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts,
                                                    const float *__restrict__ obe,
                                                    const float *__restrict__ tge, int a,
-                                                   float *row, const MarlnavParams &pr)
+                                                   float *row, const MarlnavParams &pr,
+                                                   bool &ok)
 {
     const float cap = pr.cap_distance;
     const float ox = sts[5 * a], oy = sts[5 * a + 1];
     const float dx = sts[5 * a + 2], dy = sts[5 * a + 3];
     const float td = pair_dist(ox, oy, tge[0], tge[1]);
-    const float ta = pair_angle(ox, oy, tge[0], tge[1], dx, dy, td, cap);
+    const float ta = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, td, cap, ok);
     row[0] = ta;
     row[1] = td;
     bool ob_risk = false, ob_col = false;
@@ -593,7 +604,7 @@ __device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts
     for (int j = 0; j < O; ++j) {
         const float px = obe[2 * j], py = obe[2 * j + 1];
         const float d = pair_dist(ox, oy, px, py);
-        row[2 + j] = pair_angle(ox, oy, px, py, dx, dy, d, cap);
+        row[2 + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
         row[2 + O + j] = d;
         if (TERMS) {
             ob_risk |= d < pr.ob_risk_dist;
@@ -607,7 +618,7 @@ __device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts
         const int m = j + (j >= a ? 1 : 0);
         const float px = sts[5 * m], py = sts[5 * m + 1];
         const float d = pair_dist(ox, oy, px, py);
-        row[2 + 2 * O + j] = pair_angle(ox, oy, px, py, dx, dy, d, cap);
+        row[2 + 2 * O + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
         row[2 + 2 * O + (A - 1) + j] = d;
         if (TERMS) {
             ag_risk |= d < pr.ag_risk_dist;
@@ -818,10 +829,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
         float rowv[REGROW ? D_T : 1];
         if (row_on && !(MARLNAV_ABLATE & 16)) {
             RowOut ro;
-            if constexpr (REGROW)
-                ro = observe_row_regs<A_T, O_T, !OBS_ONLY>(st + 5 * A * el, ob + 2 * S * el,
-                                                            tg + 2 * el, a, rowv, pr);
-            else
+            if constexpr (REGROW) {
+                bool ok = true;
+                ro = observe_row_regs<A_T, O_T, !OBS_ONLY, true>(
+                    st + 5 * A * el, ob + 2 * S * el, tg + 2 * el, a, rowv, pr, ok);
+                if (__builtin_expect(__ballot(!ok) != 0ull, 0) && !ok)  // IEEE redo, rare
+                    ro = observe_row_regs<A_T, O_T, !OBS_ONLY, false>(
+                        st + 5 * A * el, ob + 2 * S * el, tg + 2 * el, a, rowv, pr, ok);
+            } else
                 ro = observe_row<A_T, O_T, !OBS_ONLY>(A, O, st + 5 * A * el, ob + 2 * S * el,
                                                       tg + 2 * el, a, out_row, pr);
             if (!OBS_ONLY) {
@@ -892,10 +907,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
             // ---- observations of re-initialised envs (:105)
             if (any_fin) {
                 if (row_on && envbits[el]) {
-                    if constexpr (REGROW)
-                        observe_row_regs<A_T, O_T, false>(st + 5 * A * el, ob + 2 * S * el,
-                                                          tg + 2 * el, a, rowv, pr);
-                    else
+                    if constexpr (REGROW) {
+                        bool ok = true;
+                        observe_row_regs<A_T, O_T, false, true>(st + 5 * A * el, ob + 2 * S * el,
+                                                                tg + 2 * el, a, rowv, pr, ok);
+                        if (!ok)
+                            observe_row_regs<A_T, O_T, false, false>(
+                                st + 5 * A * el, ob + 2 * S * el, tg + 2 * el, a, rowv, pr, ok);
+                    } else
                         observe_row<A_T, O_T, false>(A, O, st + 5 * A * el, ob + 2 * S * el,
                                                      tg + 2 * el, a, out_row, pr);
                 }
