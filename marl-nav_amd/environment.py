@@ -156,6 +156,7 @@ class Env(object):
         self._step_idx = 0
         self._normalizer = None
         self._obs_norm_buffers = None
+        self._action_scaler = None
 
         self._dims = abi.MarlnavDims()
         self._cparams = abi.MarlnavParams()
@@ -262,7 +263,12 @@ class Env(object):
         values = {attr: getattr(self, attr) for attr in _PARAM_ATTRS}
         init = self._default_init_sampler if self._formation is not None else None
         self._cparams = make_cparams(values, init=init, seed=self._seed,
-                                     flags=self._cparams.flags)
+                                     flags=self._cparams.flags & ~abi.SCALE_ACTIONS)
+        if self._action_scaler is not None:
+            sc = self._action_scaler
+            self._cparams.act_scale[:] = [float(x) for x in sc.scale.float().reshape(-1)]
+            self._cparams.act_mean[:] = [float(x) for x in sc.mean.float().reshape(-1)]
+            self._cparams.flags |= abi.SCALE_ACTIONS
         self._cparams_ref = ctypes.byref(self._cparams)
         object.__setattr__(self, '_params_dirty', False)
 
@@ -383,6 +389,16 @@ class Env(object):
         if mean.numel() != D or scale.numel() != D:
             raise ValueError(f"normalizer has {mean.numel()} features, env rows have {D}")
         self._obs_norm_buffers = (mean, scale)
+
+    def attach_action_scaler(self, scaler):
+        """Have every step read raw policy actions in [-1, 1] and apply
+        ``scaler`` (an ActionScaler, utils.py:535-547) in the kernel's action
+        load: ``env.step(raw)`` then equals ``env.step(scaler(raw))`` of an
+        env without it. ``None`` detaches."""
+        if scaler is not None and (scaler.scale.numel() != 2 or scaler.mean.numel() != 2):
+            raise ValueError("ActionScaler must have 2 action components (angle, accel)")
+        self._action_scaler = scaler
+        object.__setattr__(self, '_params_dirty', True)
 
     def reset(self):
         """environment.py:70-74: marks every env for re-init and returns the

@@ -247,6 +247,29 @@ def test_fused_normalizer_and_action_scaler(pkg):
         torch.testing.assert_close(fused, ref, rtol=0, atol=0)
 
 
+def test_fused_action_scaler(pkg):
+    """§8(f) row 2: an attached ActionScaler (utils.py:535-547) applied in the
+    kernel's action load equals scaling on the host first, bit for bit."""
+    args = cli_args(num_parallel=2000, num_obstacles=3)
+    scl = pkg.ActionScaler(pkg.set_scaler_params(args, DEV))
+    fused = make_env(pkg, 2000, 3, 3, episode_len=12)
+    plain = make_env(pkg, 2000, 3, 3, episode_len=12)
+    fused.attach_action_scaler(scl)
+    g = torch.Generator().manual_seed(11)
+    for k in range(25):
+        raw = (torch.rand(2000, 3, 2, generator=g) * 2 - 1).to(DEV)
+        o1, r1, te1, tr1 = fused.step(raw)
+        o2, r2, te2, tr2 = plain.step(scl(raw))
+        assert torch.equal(fused.states, plain.states), k
+        assert torch.equal(r1, r2) and torch.equal(te1, te2) and torch.equal(tr1, tr2), k
+        assert torch.equal(o1._packed, o2._packed), k
+    fused.attach_action_scaler(None)
+    raw = torch.rand(2000, 3, 2, generator=g).to(DEV)
+    fused.step(raw)
+    plain.step(raw)
+    assert torch.equal(fused.states, plain.states)
+
+
 def test_observations_reset_and_api(pkg):
     env = make_env(pkg, 10, 3, 3)
     obs, params = env.reset()
