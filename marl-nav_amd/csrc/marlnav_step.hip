@@ -29,6 +29,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/marlnav.h"
@@ -585,16 +586,16 @@ __device__ __forceinline__ float torch_row_sum_r(const float *x, F f)
 // observe_row with compile-time shape and the packed row kept in registers
 // (row[D]); others are visited as j = 0..A-2 -> agent j + (j >= a), so
 // every row index is a compile-time constant.
+// The own row (ox, oy, dx, dy) comes in registers; the env's other agents
+// are read from sts.
 template <int A, int O, bool TERMS, bool FAST>
-__device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts,
-                                                   const float *__restrict__ obe,
-                                                   const float *__restrict__ tge, int a,
-                                                   float *row, const MarlnavParams &pr,
-                                                   bool &ok)
+__device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
+                                                  const float *__restrict__ obe,
+                                                  const float *__restrict__ tge, int a,
+                                                  float ox, float oy, float dx, float dy,
+                                                  float *row, const MarlnavParams &pr, bool &ok)
 {
     const float cap = pr.cap_distance;
-    const float ox = sts[5 * a], oy = sts[5 * a + 1];
-    const float dx = sts[5 * a + 2], dy = sts[5 * a + 3];
     const float td = pair_dist(ox, oy, tge[0], tge[1]);
     const float ta = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, td, cap, ok);
     row[0] = ta;
@@ -653,6 +654,17 @@ __device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts
         out.flags = ((ob_col || ag_col) ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u);
     }
     return out;
+}
+
+template <int A, int O, bool TERMS, bool FAST>
+__device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts,
+                                                   const float *__restrict__ obe,
+                                                   const float *__restrict__ tge, int a,
+                                                   float *row, const MarlnavParams &pr,
+                                                   bool &ok)
+{
+    return observe_row_own<A, O, TERMS, FAST>(sts, obe, tge, a, sts[5 * a], sts[5 * a + 1],
+                                              sts[5 * a + 2], sts[5 * a + 3], row, pr, ok);
 }
 
 // Store a register row of D floats with the widest aligned vector stores.
@@ -963,6 +975,401 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
 #endif
 }
 
+// ------------------------------------------------------- tile step kernel
+// The step for compile-time shapes on full, 16-byte aligned tiles (the
+// common case: every tile but a partial last one). Same tile/lane mapping
+// and phases as wave_kernel, with
+//  * staging by LDS-DMA (global_load_lds): each span of the tile is copied
+//    global -> LDS by 1-2 wave instructions, no VGPR round trip, all in
+//    flight before one vmcnt wait;
+//  * the own agent row kept in registers from the move to the observation;
+//  * per-agent reward terms packed into one 16-byte LDS slot per row;
+//  * kernel arguments that only rare paths use (re-init sources, fused
+//    normaliser, counters) read through a late kernarg pointer, so the hot
+//    path's scalar registers are not spent holding them.
+typedef __attribute__((address_space(3))) void LdsVoid;
+
+struct KArgs {
+    StepArgs a;
+    MarlnavParams p;
+};
+typedef __attribute__((address_space(4))) const KArgs KArgsK;
+
+// Kernarg pointer the compiler cannot hoist loads through.
+__device__ __forceinline__ KArgsK *kargs_late()
+{
+    KArgsK *k = (KArgsK *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return k;
+}
+
+template <class T>
+__device__ __forceinline__ T in_sgpr(T p)
+{
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+// Per-tile snapshot of the hot-path pointers and parameters, read through a
+// fresh opaque kernarg pointer each tile: nothing derived from them is
+// loop-invariant to the compiler, so a multi-tile loop keeps no per-pointer
+// induction variables or hoisted copies alive across tiles.
+struct StepPtrs {
+    float *states, *obstacles, *target, *step_num, *obs, *reward;
+    uint8_t *terminates, *terminated, *truncated;
+    const float *actions;
+};
+
+__device__ __forceinline__ StepPtrs load_ptrs(KArgsK *K)
+{
+    StepPtrs q;
+    q.states = K->a.b.states;
+    q.obstacles = K->a.b.obstacles;
+    q.target = K->a.b.target;
+    q.step_num = K->a.b.step_num;
+    q.obs = K->a.b.obs;
+    q.reward = K->a.b.reward;
+    q.terminates = K->a.b.terminates;
+    q.terminated = K->a.b.terminated;
+    q.truncated = K->a.b.truncated;
+    q.actions = K->a.b.actions;
+    return q;
+}
+
+__device__ __forceinline__ MarlnavParams load_params(KArgsK *K)
+{
+    MarlnavParams p;
+#define MARLNAV_CP(f) p.f = K->p.f
+    MARLNAV_CP(min_speed); MARLNAV_CP(max_speed); MARLNAV_CP(min_accel); MARLNAV_CP(max_accel);
+    MARLNAV_CP(trunc_after); MARLNAV_CP(risk_factor); MARLNAV_CP(distance_factor);
+    MARLNAV_CP(heading_factor); MARLNAV_CP(target_factor); MARLNAV_CP(soft_factor);
+    MARLNAV_CP(bond_factor); MARLNAV_CP(ob_risk_dist); MARLNAV_CP(ag_risk_dist);
+    MARLNAV_CP(ob_coll_dist); MARLNAV_CP(ag_coll_dist); MARLNAV_CP(agents_min_d);
+    MARLNAV_CP(agents_max_d); MARLNAV_CP(max_at_prop_d); MARLNAV_CP(max_angle_diff);
+    MARLNAV_CP(target_radius); MARLNAV_CP(cap_distance); MARLNAV_CP(bond_sharpness);
+    MARLNAV_CP(ideal_dist); MARLNAV_CP(init_dist); MARLNAV_CP(obs_range_x);
+    MARLNAV_CP(obs_mean_x); MARLNAV_CP(obs_range_y); MARLNAV_CP(obs_mean_y);
+    MARLNAV_CP(ags_dist); MARLNAV_CP(noise_std); MARLNAV_CP(angle_range);
+    MARLNAV_CP(flags); MARLNAV_CP(seed);
+    MARLNAV_CP(act_scale[0]); MARLNAV_CP(act_scale[1]);
+    MARLNAV_CP(act_mean[0]); MARLNAV_CP(act_mean[1]);
+#undef MARLNAV_CP
+    p.reserved = 0;
+    return p;
+}
+
+// global -> LDS copy of NB bytes (multiple of 4) by LDS-DMA: 16 bytes per lane
+// per instruction, then single dwords. src (16-byte aligned) and dst are
+// wave-uniform.
+template <int NB>
+__device__ __forceinline__ void glds_span(const void *src, float *dst, unsigned lane)
+{
+    constexpr int N16 = NB / 16, R4 = (NB % 16) / 4;
+#pragma unroll
+    for (int k = 0; k * 64 < N16; ++k) {
+        const char *s = in_sgpr(reinterpret_cast<const char *>(src) + k * 1024);
+        if ((k + 1) * 64 <= N16 || (int)lane < N16 - k * 64)
+            __builtin_amdgcn_global_load_lds(s + lane * 16u, (LdsVoid *)(dst + k * 256), 16, 0, 0);
+    }
+    if constexpr (R4 > 0) {
+        const char *s = in_sgpr(reinterpret_cast<const char *>(src) + N16 * 16);
+        if ((int)lane < R4)
+            __builtin_amdgcn_global_load_lds(s + lane * 4u, (LdsVoid *)(dst + N16 * 4), 4, 0, 0);
+    }
+}
+
+// plain copy of n elements (partial tiles)
+template <class T>
+__device__ __forceinline__ void copy_span(const T *__restrict__ src, T *__restrict__ dst, int n,
+                                          int lane)
+{
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (int i = lane; i < n; i += 64) dst[i] = src[i];
+}
+
+__host__ __device__ constexpr int tile_envs(int A) { return (64 / A) >= 4 ? (64 / A) & ~3 : 64 / A; }
+
+template <int A, int O>
+struct TilePlan {
+    static constexpr int W = tile_envs(A), R = W * A, D = 2 + 2 * O + 2 * (A - 1);
+    // staging buffer (floats, 16-byte aligned regions)
+    static constexpr int ST = 0;                                  // (R, 5)
+    static constexpr int ACT = (ST + R * 5 + 3) & ~3;             // (R, 2)
+    static constexpr int OB = (ACT + R * 2 + 3) & ~3;             // (W, O, 2)
+    static constexpr int TG = (OB + W * O * 2 + 3) & ~3;          // (W, 2)
+    static constexpr int SN = (TG + W * 2 + 3) & ~3;              // (W,)
+    static constexpr int TM = (SN + W + 3) & ~3;                  // (W,) bytes
+    static constexpr int STAGE = (TM + (W + 3) / 4 + 3) & ~3;
+    static constexpr int RED = STAGE;                             // (R, 4)
+    static constexpr int FLOATS = RED + 4 * R;
+};
+
+// Stage tile `tile` into `buf`: LDS-DMA for a full tile (returns without
+// waiting), plain copies for a partial last tile.
+template <int A, int O, bool OBS_ONLY>
+__device__ __forceinline__ void tile_stage(const StepPtrs &b, int64_t P, int64_t tile,
+                                           float *buf, unsigned lane)
+{
+    using TP = TilePlan<A, O>;
+    constexpr int W = TP::W, R = TP::R;
+    const int64_t e0 = tile * W;
+    if (P - e0 >= W) {
+        glds_span<R * 20>(b.states + e0 * (A * 5), buf + TP::ST, lane);
+        if (!OBS_ONLY) glds_span<R * 8>(b.actions + e0 * (A * 2), buf + TP::ACT, lane);
+        glds_span<W * O * 8>(b.obstacles + e0 * (O * 2), buf + TP::OB, lane);
+        glds_span<W * 8>(b.target + e0 * 2, buf + TP::TG, lane);
+        if (!OBS_ONLY) {
+            glds_span<W * 4>(b.step_num + e0, buf + TP::SN, lane);
+            glds_span<W>(b.terminates + e0, buf + TP::TM, lane);
+        }
+    } else {
+        const int ne = (int)(P - e0), nr = ne * A;
+        copy_span(b.states + e0 * (A * 5), buf + TP::ST, nr * 5, (int)lane);
+        if (!OBS_ONLY) copy_span(b.actions + e0 * (A * 2), buf + TP::ACT, nr * 2, (int)lane);
+        copy_span(b.obstacles + e0 * (O * 2), buf + TP::OB, ne * O * 2, (int)lane);
+        copy_span(b.target + e0 * 2, buf + TP::TG, ne * 2, (int)lane);
+        if (!OBS_ONLY) {
+            copy_span(b.step_num + e0, buf + TP::SN, ne, (int)lane);
+            copy_span(b.terminates + e0, reinterpret_cast<uint8_t *>(buf + TP::TM), ne, (int)lane);
+        }
+    }
+}
+
+// One wave per tile: stage by LDS-DMA, move, observe, reward/terminal logic,
+// re-init and re-observe finished envs, stream out.
+template <int A, int O, bool OBS_ONLY, bool NOISY = false>
+__global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
+{
+    using TP = TilePlan<A, O>;
+    constexpr int W = TP::W, D = TP::D;
+    (void)k;  // read through kargs_late()
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+#if MARLNAV_STAMPS
+    unsigned long long t_entry;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
+#endif
+    const unsigned lane = threadIdx.x & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wib;
+    const int64_t tile = gw;
+    KArgsK *K = kargs_late();
+    const int64_t P = K->a.P;
+    if (tile >= K->a.ntiles) return;
+    STAMP(0);
+    const StepPtrs b = load_ptrs(K);
+    float *wl = lds + wib * TP::FLOATS;
+    float *cur = wl;
+    float4 *red = reinterpret_cast<float4 *>(wl + TP::RED);
+    tile_stage<A, O, OBS_ONLY>(b, P, tile, cur, lane);
+    const MarlnavParams pr = load_params(K);
+    const int el = (int)lane / A, a = (int)lane - el * A;
+    unsigned c_trunc = 0, c_col = 0, c_tar = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
+    wave_sync();
+    STAMP(1);
+    {
+        const int64_t e0 = tile * W;
+        const int ne = (int)((P - e0) < W ? (P - e0) : W);
+        const int nr = ne * A;
+        const bool row_on = (int)lane < nr;
+        const bool env_on = (int)lane < ne;
+        float *st = cur + TP::ST;
+        const float *sts = st + 5 * A * el;
+        const float *obe = cur + TP::OB + 2 * O * el;
+        const float *tge = cur + TP::TG + 2 * el;
+
+        // ---- _move_agents (environment.py:113-123), own row in registers
+        float ox = st[5 * lane], oy = st[5 * lane + 1];
+        float dx = st[5 * lane + 2], dy = st[5 * lane + 3];
+        if (!OBS_ONLY) {
+            const float2 act = reinterpret_cast<const float2 *>(cur + TP::ACT)[lane];
+            float a0 = act.x, a1 = act.y;
+            if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
+                KArgsK *kl = kargs_late();
+                a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
+                a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
+            }
+            float sn, c;
+            sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+            const float ndx = c * dx + (-sn) * dy;
+            const float ndy = sn * dx + c * dy;
+            const float v = clamp_t(st[5 * lane + 4] + clamp_t(a1, pr.min_accel, pr.max_accel),
+                                    pr.min_speed, pr.max_speed);
+            ox = ox + ndx * v;
+            oy = oy + ndy * v;
+            dx = ndx;
+            dy = ndy;
+            if (row_on) {
+                float *s = st + 5 * lane;
+                s[0] = ox;
+                s[1] = oy;
+                s[2] = dx;
+                s[3] = dy;
+                s[4] = v;
+            }
+            wave_sync();
+        }
+        STAMP(2);
+
+        // ---- observations of the moved state + reward terms (:99-100)
+        float rowv[D];
+        if (row_on && !(MARLNAV_ABLATE & 16)) {
+            bool ok = true;
+            RowOut ro = observe_row_own<A, O, !OBS_ONLY, true>(sts, obe, tge, a, ox, oy, dx, dy,
+                                                               rowv, pr, ok);
+            if (__builtin_expect(__ballot(!ok) != 0ull, 0) && !ok)  // IEEE redo, rare
+                ro = observe_row_own<A, O, !OBS_ONLY, false>(sts, obe, tge, a, ox, oy, dx, dy,
+                                                             rowv, pr, ok);
+            if (!OBS_ONLY)
+                red[lane] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
+        }
+
+        STAMP(3);
+        if (!OBS_ONLY) {
+            wave_sync();
+            // ---- per-env reductions, terminal logic, masked re-init
+            bool fin = false, tr_l = false, co_l = false, ta_l = false;
+            if (env_on) {
+                const int64_t e = e0 + lane;
+                float4 rr[A];
+#pragma unroll
+                for (int i = 0; i < A; ++i) rr[i] = red[A * lane + i];
+                unsigned any_col = 0u, all_in = 1u;
+#pragma unroll
+                for (int i = 0; i < A; ++i) {
+                    const unsigned f = __float_as_uint(rr[i].z);
+                    any_col |= f & 1u;
+                    all_in &= (f >> 1) & 1u;
+                }
+                float rv[A];
+#pragma unroll
+                for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
+                const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
+                b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
+
+                float step_num = cur[TP::SN + lane] + 1.0f;        // :96
+                const bool truncated = step_num > pr.trunc_after;  // :97
+                const bool term_old = reinterpret_cast<const uint8_t *>(cur + TP::TM)[lane] != 0;
+                const bool terminated = any_col || term_old;       // :213-214
+                b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
+                b.terminated[e] = (uint8_t)terminated;
+                b.truncated[e] = (uint8_t)truncated;
+                fin = truncated || terminated;                     // :102-104
+                if (fin) {
+                    KArgsK *kl = kargs_late();
+                    MarlnavParams p;  // the fields the re-init reads
+                    p.obs_range_x = kl->p.obs_range_x;
+                    p.obs_mean_x = kl->p.obs_mean_x;
+                    p.obs_range_y = kl->p.obs_range_y;
+                    p.obs_mean_y = kl->p.obs_mean_y;
+                    p.ags_dist = kl->p.ags_dist;
+                    p.noise_std = kl->p.noise_std;
+                    p.angle_range = kl->p.angle_range;
+                    p.flags = kl->p.flags;
+                    p.seed = kl->p.seed;
+                    float *s5 = st + 5 * A * lane;
+                    float *obl = cur + TP::OB + 2 * O * lane;
+                    float *tgl = cur + TP::TG + 2 * lane;
+                    const float *fs = kl->a.b.fresh_states;
+                    float *gob = kl->a.b.obstacles;
+                    float *gtg = kl->a.b.target;
+                    if (fs) {
+                        const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
+                        if (!(p.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
+                            for (int i = 0; i < 5 * A; ++i) s5[i] = fs[e * A * 5 + i];
+                        for (int i = 0; i < 2 * O; ++i) obl[i] = fo[e * O * 2 + i];
+                        tgl[0] = ft[2 * e];
+                        tgl[1] = ft[2 * e + 1];
+                    } else {
+                        native_fresh_env<NOISY>(A, O, p, kl->a.b.formation,
+                                                (uint64_t)(kl->a.env_offset + e), kl->a.step_idx,
+                                                s5, obl, tgl);
+                    }
+                    for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
+                    gtg[2 * e] = tgl[0];
+                    gtg[2 * e + 1] = tgl[1];
+                    step_num = 0.0f;
+                }
+                b.step_num[e] = step_num;
+                tr_l = truncated;
+                co_l = any_col;
+                ta_l = all_in;
+            }
+            const uint64_t finmask = __ballot(fin);
+            c_trunc += __popcll(__ballot(tr_l));
+            c_col += __popcll(__ballot(co_l));
+            c_tar += __popcll(__ballot(ta_l));
+            STAMP(4);
+
+            // ---- observations of re-initialised envs (:105)
+            if (finmask) {
+                wave_sync();
+                if (row_on && ((finmask >> el) & 1u)) {
+                    bool ok = true;
+                    const float *s = st + 5 * lane;
+                    const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
+                    observe_row_own<A, O, false, true>(sts, obe, tge, a, rx, ry, rdx, rdy, rowv,
+                                                       pr, ok);
+                    if (!ok)
+                        observe_row_own<A, O, false, false>(sts, obe, tge, a, rx, ry, rdx, rdy,
+                                                            rowv, pr, ok);
+                }
+            }
+        }
+
+        STAMP(5);
+        // ---- stream the tile out
+        if (row_on) {
+            float *orow = in_sgpr(b.obs + e0 * (A * D)) + lane * D;
+            store_row<D>(orow, rowv);
+            if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
+                KArgsK *kl = kargs_late();
+                const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
+                float nv[D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) nv[j] = (rowv[j] - mean[j]) / scale[j];
+                store_row<D>(kl->a.b.obs_norm + (e0 * A + lane) * D, nv);
+            }
+        }
+        if (!OBS_ONLY) {
+            wave_sync();
+            float *gst = in_sgpr(b.states + e0 * (A * 5));
+            if (ne == W) {
+                constexpr int N16 = TP::R * 5 / 4;  // R*5 is a multiple of 4 (W % 4 == 0)
+#pragma unroll
+                for (int kk = 0; kk * 64 < N16; ++kk) {
+                    const int i = kk * 64 + (int)lane;
+                    if ((kk + 1) * 64 <= N16 || i < N16)
+                        reinterpret_cast<float4 *>(gst)[i] = reinterpret_cast<const float4 *>(st)[i];
+                }
+            } else {
+                for (int i = (int)lane; i < nr * 5; i += 64) gst[i] = st[i];
+            }
+        }
+    }
+    STAMP(6);
+    if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
+        // this wave's own slots: contention-free, fire-and-forget
+        KArgsK *kl = kargs_late();
+        uint64_t *cnt = kl->a.b.counters;
+        const int64_t slots = kl->a.waves;
+        if (cnt) {
+            if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + gw], (unsigned long long)c_trunc);
+            if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + gw], (unsigned long long)c_col);
+            if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + gw], (unsigned long long)c_tar);
+        }
+    }
+#if MARLNAV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(7);
+    if (lane == 0) {
+        g_stamps[(size_t)gw * 24 + 16] = t_entry;
+        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+    }
+#endif
+}
+
 // ----------------------------------------------------- native reinit kernel
 __global__ void reinit_all_kernel(int64_t P, int A, int S, int64_t env_offset, uint64_t sidx,
                                   MarlnavParams pr, const float *__restrict__ formation,
@@ -1062,6 +1469,64 @@ const KernelPair kVariants[] = {
      wave_kernel<16, 32, false, true>},
 };
 
+// LDS-DMA tile kernels (tile_kernel) for these shapes; MARLNAV_TILE=0 builds
+// without them (A/B timing against wave_kernel)
+#ifndef MARLNAV_TILE
+#define MARLNAV_TILE 1
+#endif
+using TileFn = void (*)(KArgs);
+
+struct TilePair {
+    int A, O;
+    TileFn step, obs, noisy;
+    size_t lds;  // bytes per block
+};
+
+#define MARLNAV_TILE_VARIANT(A, O)                                                        \
+    {A, O, tile_kernel<A, O, false>, tile_kernel<A, O, true>, tile_kernel<A, O, false, true>, \
+     (size_t)TilePlan<A, O>::FLOATS * 4 * kWavesPerBlock}
+const TilePair kTileVariants[] = {
+    MARLNAV_TILE_VARIANT(3, 3),
+    MARLNAV_TILE_VARIANT(3, 8),
+    MARLNAV_TILE_VARIANT(3, 1),
+    MARLNAV_TILE_VARIANT(2, 1),
+};
+#undef MARLNAV_TILE_VARIANT
+
+bool aligned(const void *p, uintptr_t n) { return (reinterpret_cast<uintptr_t>(p) & (n - 1)) == 0; }
+
+// tile_kernel applies: a compiled shape, obstacle_stride == O and the
+// alignment its LDS-DMA staging and vector stores assume
+const TilePair *select_tile(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only)
+{
+    if (!MARLNAV_TILE || d->obstacle_stride != d->num_obstacles) return nullptr;
+    const TilePair *t = nullptr;
+    for (const TilePair &v : kTileVariants)
+        if (v.A == d->num_agents && v.O == d->num_obstacles) t = &v;
+    if (!t || tile_envs(t->A) != pick_wave_envs(t->A, t->O, t->O)) return nullptr;
+    if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
+        !aligned(b.obs, 16))
+        return nullptr;
+    if (!obs_only && (!aligned(b.actions, 16) || !aligned(b.step_num, 16) ||
+                      !aligned(b.terminates, 4)))
+        return nullptr;
+    return t;
+}
+
+int launch_tile(TileFn fn, size_t lds, const Launch &L, const StepArgs &args,
+                const MarlnavParams &pr, void *stream, const char *what)
+{
+    KArgs ka;
+    ka.a = args;
+    ka.p = pr;
+    void *kargs[] = {&ka};
+    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)L.blocks),
+                                   dim3(64 * kWavesPerBlock), kargs, lds, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+    return 0;
+}
+
 bool has_variant(int A, int O)
 {
     for (const KernelPair &k : kVariants)
@@ -1146,8 +1611,11 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavSte
     StepArgs args = make_args(d, L);
     args.b = *b;
     args.step_idx = step_idx;
-    const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
     const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
+    if (const TilePair *t = select_tile(d, *b, false))
+        return launch_tile(noisy ? t->noisy : t->step, t->lds, L, args, *pr, stream,
+                           "marlnav_step");
+    const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
     return launch(noisy ? k.noisy : k.step, L, args, *pr, stream, "marlnav_step");
 }
 
@@ -1166,6 +1634,8 @@ int marlnav_observe(const MarlnavDims *d, const float *states, const float *obst
     MarlnavParams pr;
     memset(&pr, 0, sizeof(pr));
     pr.cap_distance = 0.1f;  // environment.py:65
+    if (const TilePair *t = select_tile(d, args.b, true))
+        return launch_tile(t->obs, t->lds, L, args, pr, stream, "marlnav_observe");
     return launch(select_kernels(d->num_agents, d->num_obstacles).obs, L, args, pr, stream,
                   "marlnav_observe");
 }

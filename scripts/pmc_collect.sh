@@ -14,8 +14,10 @@ PASSES=(
  "WRITE_SIZE GRBM_GUI_ACTIVE"
  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_LDS SQ_IFETCH"
 )
+ONLY=${ONLY:-01234}   # which passes to run
 i=0
 for p in "${PASSES[@]}"; do
+  case "$ONLY" in *$i*) ;; *) i=$((i+1)); continue;; esac
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $p --output-format csv -d $OUT/p$i -o run -- python scripts/pmc_run.py $CFG 40 > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
   case $rc in 0|1) ;; *) exit $rc;; esac
