@@ -22,6 +22,7 @@ Differences from the reference, all deliberate:
 """
 import ctypes
 import math
+import sys
 
 import torch
 
@@ -157,6 +158,10 @@ class Env(object):
         self._normalizer = None
         self._obs_norm_buffers = None
         self._action_scaler = None
+        self._buf_gen = 0          # bumped whenever a device buffer is replaced
+        self._out_pool = []        # reusable step outputs (_OutputSet)
+        self._out_next = 0
+        self._last_out = None
 
         self._dims = abi.MarlnavDims()
         self._cparams = abi.MarlnavParams()
@@ -235,6 +240,7 @@ class Env(object):
         if target is not None:
             object.__setattr__(self, '_target', own(target, (P, 1, 2)))
         self._update_dims()
+        self.__dict__['_buf_gen'] = self.__dict__.get('_buf_gen', 0) + 1
 
     def _update_dims(self):
         S = int(self._obstacles.shape[1])
@@ -251,6 +257,7 @@ class Env(object):
         self._act_shape = (self.num_parallel, self.num_agents, 2)
         O = d.num_obstacles
         self._split = [1, 1, O, O, self.num_agents - 1, self.num_agents - 1]
+        self.__dict__['_out_pool'] = []  # output shapes may have changed
         if hasattr(self, '_counters') and old != (d.num_agents, d.num_obstacles, S):
             totals = self._counter_totals()
             self._counters = torch.zeros(3, self._slots(), dtype=torch.int64,
@@ -277,7 +284,7 @@ class Env(object):
                            dtype=_F32, device=self.device)
 
     def _wrap_obs(self, packed, normalized=None):
-        o = tuple.__new__(_PackedObservations, torch.split(packed, self._split, 2))
+        o = tuple.__new__(_PackedObservations, packed.split_with_sizes(self._split, 2))
         o._packed = packed
         o._normalized = normalized
         o._normalizer = self._normalizer
@@ -315,6 +322,7 @@ class Env(object):
     @_step_num.setter
     def _step_num(self, value):
         self.__dict__['_step_num_t'] = self._dev_f32(value, (self.num_parallel,))
+        self.__dict__['_buf_gen'] = self.__dict__.get('_buf_gen', 0) + 1
 
     @property
     def _terminates(self):
@@ -326,6 +334,7 @@ class Env(object):
         if tuple(t.shape) != (self.num_parallel,):
             raise ValueError(f"_terminates must be ({self.num_parallel},)")
         self.__dict__['_terminates_t'] = t
+        self.__dict__['_buf_gen'] = self.__dict__.get('_buf_gen', 0) + 1
 
     @property
     def _reinit_mask(self):
@@ -380,6 +389,8 @@ class Env(object):
         """Have every step also write ``normalizer``'s output (utils.py:519-532)
         from the kernel; ``normalizer(obs)`` then returns it without work."""
         self._normalizer = normalizer
+        self._out_pool = []
+        self._buf_gen += 1
         if normalizer is None:
             self._obs_norm_buffers = None
             return
@@ -428,9 +439,45 @@ class Env(object):
             raise ValueError(f"actions must be {self._act_shape}, got {tuple(actions.shape)}")
         return actions
 
+    def _take_outputs(self):
+        """This step's output set: a pooled one nothing references any more,
+        else a new allocation (pooled while the pool is small)."""
+        pool = self._out_pool
+        capturing = torch.cuda.is_current_stream_capturing()
+        if pool and not capturing:
+            last = self._last_out
+            n = len(pool)
+            i = self._out_next
+            for _ in range(2 if n > 1 else 1):
+                out = pool[i]
+                i = i + 1 if i + 1 < n else 0
+                if out is not last and out.free():
+                    self._out_next = i
+                    return out
+        out = _OutputSet(self)
+        if not capturing and len(pool) < _POOL_MAX:
+            pool.append(out)
+            out.arm()
+        return out
+
+    def _fill_buffers(self, b):
+        """Point a step-buffer struct at the env's current device buffers."""
+        b.states = self._states.data_ptr()
+        b.obstacles = self._obstacles.data_ptr()
+        b.target = self._target.data_ptr()
+        b.step_num = self.__dict__['_step_num_t'].data_ptr()
+        b.terminates = self.__dict__['_terminates_t'].data_ptr()
+        b.counters = self._counters.data_ptr()
+        b.formation = self._formation.data_ptr() if self._formation is not None else None
+        if self._obs_norm_buffers is not None:
+            b.norm_mean = self._obs_norm_buffers[0].data_ptr()
+            b.norm_scale = self._obs_norm_buffers[1].data_ptr()
+
     def step(self, actions):
         """environment.py:92-107: returns (Observations, rewards (P,),
-        terminated (P,) bool, truncated (P,) bool)."""
+        terminated (P,) bool, truncated (P,) bool). The returned tensors are
+        never aliased with any tensor still referenced from a previous step;
+        their memory is recycled only once nothing refers to it."""
         if self._params_dirty:
             self._sync_params()
         dev = self.device
@@ -438,48 +485,34 @@ class Env(object):
                 and actions.device == dev and actions.shape == self._act_shape
                 and actions.is_contiguous()):
             actions = self._coerce_actions(actions)
-        P = self.num_parallel
-        obs = torch.empty(self._obs_shape, dtype=_F32, device=dev)
-        reward = torch.empty(P, dtype=_F32, device=dev)
-        terminated = torch.empty(P, dtype=torch.bool, device=dev)
-        truncated = torch.empty(P, dtype=torch.bool, device=dev)
-        b = self._bufs
-        b.states = self._states.data_ptr()
-        b.obstacles = self._obstacles.data_ptr()
-        b.target = self._target.data_ptr()
-        b.step_num = self.__dict__['_step_num_t'].data_ptr()
-        b.terminates = self.__dict__['_terminates_t'].data_ptr()
+        d = self.__dict__
+        out = self._take_outputs()
+        b = out.bufs
+        if out.gen != d['_buf_gen']:
+            self._fill_buffers(b)
+            out.gen = d['_buf_gen']
         b.actions = actions.data_ptr()
-        b.obs = obs.data_ptr()
-        b.reward = reward.data_ptr()
-        b.terminated = terminated.data_ptr()
-        b.truncated = truncated.data_ptr()
-        b.counters = self._counters.data_ptr()
         cp = self._cparams
         flags = cp.flags & ~(abi.FRESH_STATES_FROM_MOVED | abi.WRITE_OBS_NORM)
         keep = None
         if self._rng == 'native' and self._init_sampler is self._default_init_sampler:
-            b.fresh_states = b.fresh_obstacles = b.fresh_target = None
-            b.formation = self._formation.data_ptr()
+            if out.fresh:
+                b.fresh_states = b.fresh_obstacles = b.fresh_target = None
+                out.fresh = False
         else:
+            P = self.num_parallel
             fs, fo, ft = self._init_sampler()                # environment.py:78
             S = self._obstacles.shape[1]
             keep = (self._dev_f32(fs, (P, self.num_agents, 5)),
                     self._dev_f32(fo, (P, S, 2)), self._dev_f32(ft, (P, 1, 2)))
             b.fresh_states, b.fresh_obstacles, b.fresh_target = (t.data_ptr() for t in keep)
-            b.formation = None
+            out.fresh = True
             if self._mock_alias:
                 flags |= abi.FRESH_STATES_FROM_MOVED
-        normalized = None
-        if self._obs_norm_buffers is not None:
-            normalized = torch.empty(self._obs_shape, dtype=_F32, device=dev)
-            b.obs_norm = normalized.data_ptr()
-            b.norm_mean = self._obs_norm_buffers[0].data_ptr()
-            b.norm_scale = self._obs_norm_buffers[1].data_ptr()
+        if out.normalized is not None:
             flags |= abi.WRITE_OBS_NORM
         cp.flags = flags
-        d = self.__dict__
-        rc = self._lib.marlnav_step(self._dims_ref, self._cparams_ref, self._bufs_ref,
+        rc = self._lib.marlnav_step(self._dims_ref, self._cparams_ref, out.bufs_ref,
                                     d['_step_idx'], _stream_handle(dev))
         if rc:
             abi.check(rc, self._lib)
@@ -491,10 +524,81 @@ class Env(object):
             init = self._init_sampler
             if isinstance(init, MockInitializer):
                 init.states = self._states.clone()
-        d['_last_finished'] = (terminated, truncated)
+        d['_last_out'] = out
+        d['_last_finished'] = (out.terminated, out.truncated)
         d['_reinit_mask_t'] = None
         del keep
-        return self._wrap_obs(obs, normalized), reward, terminated, truncated
+        return out.obs, out.reward, out.terminated, out.truncated
+
+
+_POOL_MAX = 4
+
+
+class _OutputSet(object):
+    """The output tensors of one step carved from ONE device allocation:
+    packed observations (and the fused-normalizer copy), reward, terminated,
+    truncated, plus the Observations tuple of views and a step-buffer struct
+    pointing at them. A pooled set is handed out again only when nothing
+    outside the env refers to it: no extra Python reference to any object
+    it handed out and no other tensor viewing its storage (so a caller that
+    keeps any output, or a view of one, never sees it overwritten)."""
+    __slots__ = ('obs', 'packed', 'normalized', 'reward', 'terminated', 'truncated',
+                 'bufs', 'bufs_ref', 'gen', 'fresh', '_cdata', '_objs', '_base_use',
+                 '_base_refs')
+
+    def __init__(self, env):
+        P, A, D = env._obs_shape
+        dev = env.device
+        nobs = P * A * D * 4
+        norm = env._obs_norm_buffers is not None
+
+        def up(n):
+            return (n + 255) & ~255
+        o_norm = up(nobs)
+        o_rew = o_norm + (up(nobs) if norm else 0)
+        o_term = o_rew + up(4 * P)
+        o_trunc = o_term + up(P)
+        buf = torch.empty(o_trunc + up(P), dtype=torch.uint8, device=dev)
+        self.packed = buf[:nobs].view(_F32).view(P, A, D)
+        self.normalized = buf[o_norm:o_norm + nobs].view(_F32).view(P, A, D) if norm else None
+        self.reward = buf[o_rew:o_rew + 4 * P].view(_F32)
+        self.terminated = buf[o_term:o_term + P].view(torch.bool)
+        self.truncated = buf[o_trunc:o_trunc + P].view(torch.bool)
+        self.obs = env._wrap_obs(self.packed, self.normalized)
+        self._cdata = buf.untyped_storage()._cdata
+        del buf
+        self.bufs = abi.MarlnavStepBuffers()
+        self.bufs_ref = ctypes.byref(self.bufs)
+        b = self.bufs
+        b.obs = self.packed.data_ptr()
+        b.reward = self.reward.data_ptr()
+        b.terminated = self.terminated.data_ptr()
+        b.truncated = self.truncated.data_ptr()
+        if norm:
+            b.obs_norm = self.normalized.data_ptr()
+        self.gen = -1
+        self.fresh = True
+        self._objs = None
+
+    def arm(self):
+        """Record the reference counts that mean 'held by the pool only'."""
+        objs = (self.obs, self.packed, self.reward, self.terminated,
+                self.truncated) + tuple(self.obs)
+        if self.normalized is not None:
+            objs = objs + (self.normalized,)
+        self._objs = objs
+        self._base_use = torch._C._storage_Use_Count(self._cdata)
+        self._base_refs = _refcounts(objs)
+
+    def free(self):
+        return (torch._C._storage_Use_Count(self._cdata) == self._base_use
+                and _refcounts(self._objs) == self._base_refs)
+
+
+def _refcounts(objs):
+    # one code path for the baseline and the check: the counts include this
+    # function's own temporary references identically
+    return [sys.getrefcount(x) for x in objs]
 
 
 class _PackedObservations(Observations):

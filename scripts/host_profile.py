@@ -48,4 +48,13 @@ for _ in range(3000):
     env.step(acts)
 pr.disable()
 torch.cuda.synchronize()
-pstats.Stats(pr).sort_stats("tottime").print_stats(14)
+pstats.Stats(pr).sort_stats("tottime").print_stats(20)
+# the launch alone: ctypes call of marlnav_step with pre-set buffers
+import numpy as np
+print("is_capturing        %.2f us" % t(torch.cuda.is_current_stream_capturing))
+print("take_outputs        %.2f us" % t(env._take_outputs))
+o = env._out_pool[0]
+print("set.free            %.2f us" % t(o.free))
+o2 = env._take_outputs()
+print("marlnav_step call   %.2f us" % t(lambda: lib.marlnav_step(env._dims_ref, env._cparams_ref, o2.bufs_ref, 1, torch._C._cuda_getCurrentRawStream(0))))
+print("tiny torch op       %.2f us" % t(lambda: obs.add_(0)))

@@ -305,3 +305,33 @@ def test_sharded_native_init_is_invariant(pkg):
     torch.testing.assert_close(full.states, torch.cat([a.states, b.states]), rtol=0, atol=0)
     torch.testing.assert_close(full.obstacles, torch.cat([a.obstacles, b.obstacles]),
                                rtol=0, atol=0)
+
+
+def test_step_outputs_never_alias_live_tensors(pkg):
+    """Env.step recycles output memory only when nothing refers to it: kept
+    outputs, kept views and kept Observations tuples are never overwritten."""
+    env = make_env(pkg, 777, 3, 3, episode_len=9)
+    acts = [torch.rand(777, 3, 2, device=DEV) - 0.5 for _ in range(4)]
+    kept = []
+    for k in range(12):
+        obs, rew, term, trunc = env.step(acts[k % 4])
+        if k % 3 == 0:
+            kept.append(("obs", obs, obs._packed.clone()))
+        elif k % 3 == 1:
+            kept.append(("view", obs.obstacles_distances[5:9], obs.obstacles_distances[5:9].clone()))
+            kept.append(("rew", rew, rew.clone()))
+        else:
+            kept.append(("term", term, term.clone()))
+            kept.append(("trunc", trunc, trunc.clone()))
+        del obs, rew, term, trunc
+    torch.cuda.synchronize()
+    for what, live, snap in kept:
+        cur = live._packed if what == "obs" else live
+        assert torch.equal(cur, snap), what
+    # nothing kept: the memory is recycled (bounded pool)
+    ptrs = set()
+    for k in range(10):
+        o, r, te, tr = env.step(acts[k % 4])
+        ptrs.add(o._packed.data_ptr())
+        del o, r, te, tr
+    assert len(ptrs) <= 4

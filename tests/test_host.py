@@ -1,0 +1,43 @@
+"""Host-side logic of the drop-in Env that needs no GPU: the step-output
+recycling rule (marl-nav_amd/environment.py _OutputSet)."""
+import importlib
+
+import torch
+
+envmod = importlib.import_module("marl-nav_amd.environment")
+
+
+class _Stub:
+    """The attributes _OutputSet reads from an Env."""
+    _obs_shape = (10, 3, 12)
+    device = torch.device("cpu")
+    _obs_norm_buffers = None
+    _split = [1, 1, 3, 3, 2, 2]
+    _normalizer = None
+    _wrap_obs = envmod.Env._wrap_obs
+
+
+def test_output_set_layout():
+    s = envmod._OutputSet(_Stub())
+    assert s.packed.shape == (10, 3, 12) and s.packed.dtype == torch.float32
+    assert s.reward.shape == (10,) and s.terminated.dtype == torch.bool
+    assert [tuple(f.shape) for f in s.obs] == [(10, 3, 1), (10, 3, 1), (10, 3, 3), (10, 3, 3),
+                                               (10, 3, 2), (10, 3, 2)]
+    # one allocation, disjoint regions
+    regions = sorted((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size())
+                     for t in (s.packed, s.reward, s.terminated, s.truncated))
+    assert all(a[1] <= b[0] for a, b in zip(regions, regions[1:]))
+    assert s.obs._packed is s.packed
+
+
+def test_output_set_is_free_only_when_unreferenced():
+    s = envmod._OutputSet(_Stub())
+    s.arm()
+    assert s.free()
+    held = [lambda: s.reward, lambda: s.obs, lambda: s.obs[3], lambda: s.obs.target_angle[2:4],
+            lambda: s.packed.view(-1), lambda: s.truncated[1:], lambda: (s.obs, s.reward)]
+    for make in held:
+        x = make()
+        assert not s.free()
+        del x
+        assert s.free()
