@@ -45,7 +45,7 @@ constexpr int kObsTileMax = 2304;       // floats of packed obs staged per wave
 
 // Timing-only ablation builds (scripts/kbench.py; never shipped, results
 // wrong by construction): 1 no acos, 2 fp32 fast sin/cos, 4 fast division,
-// 8 fast sqrt, 16 no observation math at all.
+// 8 fast sqrt, 16 no observation math at all, 64 tile kernel returns at entry.
 #ifndef MARLNAV_ABLATE
 #define MARLNAV_ABLATE 0
 #endif
@@ -1089,9 +1089,17 @@ __device__ __forceinline__ void copy_span(const T *__restrict__ src, T *__restri
 
 __host__ __device__ constexpr int tile_envs(int A) { return (64 / A) >= 4 ? (64 / A) & ~3 : 64 / A; }
 
-template <int A, int O>
+__host__ __device__ constexpr int tile_kernel_envs(int A, int rpl) { return rpl * tile_envs(A); }
+
+// Wave tile of the tile kernels: W = RPL * tile_envs(A) envs; lane l < L
+// (L = tile_envs(A) * A) owns agent rows l, l + L, ... (RPL of them; the
+// same agent index in each, as L % A == 0), and lane e < W owns env e in the
+// per-env phase.
+template <int A, int O, int RPL_ = 1>
 struct TilePlan {
-    static constexpr int W = tile_envs(A), R = W * A, D = 2 + 2 * O + 2 * (A - 1);
+    static constexpr int RPL = RPL_;
+    static constexpr int L = tile_envs(A) * A;
+    static constexpr int W = RPL * tile_envs(A), R = W * A, D = 2 + 2 * O + 2 * (A - 1);
     // staging buffer (floats, 16-byte aligned regions)
     static constexpr int ST = 0;                                  // (R, 5)
     static constexpr int ACT = (ST + R * 5 + 3) & ~3;             // (R, 2)
@@ -1102,15 +1110,16 @@ struct TilePlan {
     static constexpr int STAGE = (TM + (W + 3) / 4 + 3) & ~3;
     static constexpr int RED = STAGE;                             // (R, 4)
     static constexpr int FLOATS = RED + 4 * R;
+    static_assert(W <= 64, "one lane per env in the per-env phase");
 };
 
 // Stage tile `tile` into `buf`: LDS-DMA for a full tile (returns without
 // waiting), plain copies for a partial last tile.
-template <int A, int O, bool OBS_ONLY>
+template <int A, int O, bool OBS_ONLY, int RPL>
 __device__ __forceinline__ void tile_stage(const StepPtrs &b, int64_t P, int64_t tile,
                                            float *buf, unsigned lane)
 {
-    using TP = TilePlan<A, O>;
+    using TP = TilePlan<A, O, RPL>;
     constexpr int W = TP::W, R = TP::R;
     const int64_t e0 = tile * W;
     if (P - e0 >= W) {
@@ -1136,14 +1145,20 @@ __device__ __forceinline__ void tile_stage(const StepPtrs &b, int64_t P, int64_t
 }
 
 // One wave per tile: stage by LDS-DMA, move, observe, reward/terminal logic,
-// re-init and re-observe finished envs, stream out.
-template <int A, int O, bool OBS_ONLY, bool NOISY = false>
+// re-init and re-observe finished envs, stream out. Each lane's RPL rows are
+// independent work the compiler interleaves: RPL = 1 gives the most waves
+// (shortest per-wave chain; best while the grid is one round of waves),
+// RPL = 2 halves the per-env fixed cost (best once waves queue up).
+template <int A, int O, bool OBS_ONLY, bool NOISY, int RPL>
 __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
 {
-    using TP = TilePlan<A, O>;
-    constexpr int W = TP::W, D = TP::D;
+    using TP = TilePlan<A, O, RPL>;
+    constexpr int W = TP::W, D = TP::D, L = TP::L;
     (void)k;  // read through kargs_late()
     extern __shared__ __attribute__((aligned(16))) float lds[];
+#if MARLNAV_ABLATE & 64
+    return;  // launch-overhead probe
+#endif
 #if MARLNAV_STAMPS
     unsigned long long t_entry;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
@@ -1160,7 +1175,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
     float *wl = lds + wib * TP::FLOATS;
     float *cur = wl;
     float4 *red = reinterpret_cast<float4 *>(wl + TP::RED);
-    tile_stage<A, O, OBS_ONLY>(b, P, tile, cur, lane);
+    tile_stage<A, O, OBS_ONLY, RPL>(b, P, tile, cur, lane);
     const MarlnavParams pr = load_params(K);
     const int el = (int)lane / A, a = (int)lane - el * A;
     unsigned c_trunc = 0, c_col = 0, c_tar = 0;
@@ -1171,57 +1186,93 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
         const int64_t e0 = tile * W;
         const int ne = (int)((P - e0) < W ? (P - e0) : W);
         const int nr = ne * A;
-        const bool row_on = (int)lane < nr;
         const bool env_on = (int)lane < ne;
         float *st = cur + TP::ST;
-        const float *sts = st + 5 * A * el;
-        const float *obe = cur + TP::OB + 2 * O * el;
-        const float *tge = cur + TP::TG + 2 * el;
+        // row k of this lane: index lane + k*L, env el + k*(L/A)
+        bool row_on[RPL];
+        int rix[RPL], rel[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            rix[q] = (int)lane + q * L;
+            rel[q] = el + q * (L / A);
+            row_on[q] = (int)lane < L && rix[q] < nr;
+        }
 
-        // ---- _move_agents (environment.py:113-123), own row in registers
-        float ox = st[5 * lane], oy = st[5 * lane + 1];
-        float dx = st[5 * lane + 2], dy = st[5 * lane + 3];
+        // ---- _move_agents (environment.py:113-123), own rows in registers
+        float ox[RPL], oy[RPL], dx[RPL], dy[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const float *s = st + 5 * rix[q];
+            ox[q] = s[0];
+            oy[q] = s[1];
+            dx[q] = s[2];
+            dy[q] = s[3];
+        }
         if (!OBS_ONLY) {
-            const float2 act = reinterpret_cast<const float2 *>(cur + TP::ACT)[lane];
-            float a0 = act.x, a1 = act.y;
-            if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
-                KArgsK *kl = kargs_late();
-                a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
-                a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
-            }
-            float sn, c;
-            sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
-            const float ndx = c * dx + (-sn) * dy;
-            const float ndy = sn * dx + c * dy;
-            const float v = clamp_t(st[5 * lane + 4] + clamp_t(a1, pr.min_accel, pr.max_accel),
-                                    pr.min_speed, pr.max_speed);
-            ox = ox + ndx * v;
-            oy = oy + ndy * v;
-            dx = ndx;
-            dy = ndy;
-            if (row_on) {
-                float *s = st + 5 * lane;
-                s[0] = ox;
-                s[1] = oy;
-                s[2] = dx;
-                s[3] = dy;
-                s[4] = v;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const float2 act = reinterpret_cast<const float2 *>(cur + TP::ACT)[rix[q]];
+                float a0 = act.x, a1 = act.y;
+                if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
+                    KArgsK *kl = kargs_late();
+                    a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
+                    a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
+                }
+                float sn, c;
+                sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+                const float ndx = c * dx[q] + (-sn) * dy[q];
+                const float ndy = sn * dx[q] + c * dy[q];
+                float *s = st + 5 * rix[q];
+                const float v = clamp_t(s[4] + clamp_t(a1, pr.min_accel, pr.max_accel),
+                                        pr.min_speed, pr.max_speed);
+                ox[q] = ox[q] + ndx * v;
+                oy[q] = oy[q] + ndy * v;
+                dx[q] = ndx;
+                dy[q] = ndy;
+                if (row_on[q]) {
+                    s[0] = ox[q];
+                    s[1] = oy[q];
+                    s[2] = dx[q];
+                    s[3] = dy[q];
+                    s[4] = v;
+                }
             }
             wave_sync();
         }
         STAMP(2);
 
         // ---- observations of the moved state + reward terms (:99-100)
-        float rowv[D];
-        if (row_on && !(MARLNAV_ABLATE & 16)) {
-            bool ok = true;
-            RowOut ro = observe_row_own<A, O, !OBS_ONLY, true>(sts, obe, tge, a, ox, oy, dx, dy,
-                                                               rowv, pr, ok);
-            if (__builtin_expect(__ballot(!ok) != 0ull, 0) && !ok)  // IEEE redo, rare
-                ro = observe_row_own<A, O, !OBS_ONLY, false>(sts, obe, tge, a, ox, oy, dx, dy,
-                                                             rowv, pr, ok);
-            if (!OBS_ONLY)
-                red[lane] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
+        float rowv[RPL][D];
+        if (!(MARLNAV_ABLATE & 16) && (int)lane < L) {
+            bool ok[RPL];
+            RowOut ro[RPL];
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                ok[q] = true;
+                ro[q] = observe_row_own<A, O, !OBS_ONLY, true>(
+                    st + 5 * A * rel[q], cur + TP::OB + 2 * O * rel[q], cur + TP::TG + 2 * rel[q],
+                    a, ox[q], oy[q], dx[q], dy[q], rowv[q], pr, ok[q]);
+                ok[q] = ok[q] || !row_on[q];  // rows past the tile: garbage, unused
+            }
+            bool all_ok = true;
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) all_ok = all_ok && ok[q];
+            if (__builtin_expect(__ballot(!all_ok) != 0ull, 0)) {  // IEEE redo, rare
+#pragma unroll
+                for (int q = 0; q < RPL; ++q)
+                    if (!ok[q])
+                        ro[q] = observe_row_own<A, O, !OBS_ONLY, false>(
+                            st + 5 * A * rel[q], cur + TP::OB + 2 * O * rel[q],
+                            cur + TP::TG + 2 * rel[q], a, ox[q], oy[q], dx[q], dy[q], rowv[q], pr,
+                            ok[q]);
+            }
+            if (!OBS_ONLY) {
+#pragma unroll
+                for (int q = 0; q < RPL; ++q)
+                    if (row_on[q])
+                        red[rix[q]] = make_float4(ro[q].r_miss, ro[q].r_hit,
+                                                  __uint_as_float(ro[q].flags), 0.0f);
+            }
         }
 
         STAMP(3);
@@ -1304,31 +1355,40 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
             // ---- observations of re-initialised envs (:105)
             if (finmask) {
                 wave_sync();
-                if (row_on && ((finmask >> el) & 1u)) {
-                    bool ok = true;
-                    const float *s = st + 5 * lane;
-                    const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
-                    observe_row_own<A, O, false, true>(sts, obe, tge, a, rx, ry, rdx, rdy, rowv,
-                                                       pr, ok);
-                    if (!ok)
-                        observe_row_own<A, O, false, false>(sts, obe, tge, a, rx, ry, rdx, rdy,
-                                                            rowv, pr, ok);
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    if (row_on[q] && ((finmask >> rel[q]) & 1u)) {
+                        bool ok = true;
+                        const float *s = st + 5 * rix[q];
+                        const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
+                        const float *sts = st + 5 * A * rel[q];
+                        const float *obe = cur + TP::OB + 2 * O * rel[q];
+                        const float *tge = cur + TP::TG + 2 * rel[q];
+                        observe_row_own<A, O, false, true>(sts, obe, tge, a, rx, ry, rdx, rdy,
+                                                           rowv[q], pr, ok);
+                        if (!ok)
+                            observe_row_own<A, O, false, false>(sts, obe, tge, a, rx, ry, rdx,
+                                                                rdy, rowv[q], pr, ok);
+                    }
                 }
             }
         }
 
         STAMP(5);
         // ---- stream the tile out
-        if (row_on) {
-            float *orow = in_sgpr(b.obs + e0 * (A * D)) + lane * D;
-            store_row<D>(orow, rowv);
-            if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
-                KArgsK *kl = kargs_late();
-                const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
-                float nv[D];
+        float *obase = in_sgpr(b.obs + e0 * (A * D));
 #pragma unroll
-                for (int j = 0; j < D; ++j) nv[j] = (rowv[j] - mean[j]) / scale[j];
-                store_row<D>(kl->a.b.obs_norm + (e0 * A + lane) * D, nv);
+        for (int q = 0; q < RPL; ++q) {
+            if (row_on[q]) {
+                store_row<D>(obase + rix[q] * D, rowv[q]);
+                if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
+                    KArgsK *kl = kargs_late();
+                    const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
+                    float nv[D];
+#pragma unroll
+                    for (int j = 0; j < D; ++j) nv[j] = (rowv[q][j] - mean[j]) / scale[j];
+                    store_row<D>(kl->a.b.obs_norm + (e0 * A + rix[q]) * D, nv);
+                }
             }
         }
         if (!OBS_ONLY) {
@@ -1475,16 +1535,24 @@ const KernelPair kVariants[] = {
 #define MARLNAV_TILE 1
 #endif
 using TileFn = void (*)(KArgs);
+// RPL=1 waves (one per 64/A-env tile) from which RPL=2 is used
+constexpr int64_t kRpl2Waves = 49152;  // measured crossover ~0.5-1M envs at A=3
 
-struct TilePair {
-    int A, O;
+struct TileSet {
     TileFn step, obs, noisy;
     size_t lds;  // bytes per block
 };
 
-#define MARLNAV_TILE_VARIANT(A, O)                                                        \
-    {A, O, tile_kernel<A, O, false>, tile_kernel<A, O, true>, tile_kernel<A, O, false, true>, \
-     (size_t)TilePlan<A, O>::FLOATS * 4 * kWavesPerBlock}
+struct TilePair {
+    int A, O;
+    TileSet rpl[2];  // 1 and 2 rows per lane
+};
+
+#define MARLNAV_TILE_SET(A, O, R)                                                   \
+    {tile_kernel<A, O, false, false, R>, tile_kernel<A, O, true, false, R>,         \
+     tile_kernel<A, O, false, true, R>, (size_t)TilePlan<A, O, R>::FLOATS * 4 * kWavesPerBlock}
+#define MARLNAV_TILE_VARIANT(A, O) \
+    {A, O, {MARLNAV_TILE_SET(A, O, 1), MARLNAV_TILE_SET(A, O, 2)}}
 const TilePair kTileVariants[] = {
     MARLNAV_TILE_VARIANT(3, 3),
     MARLNAV_TILE_VARIANT(3, 8),
@@ -1492,6 +1560,20 @@ const TilePair kTileVariants[] = {
     MARLNAV_TILE_VARIANT(2, 1),
 };
 #undef MARLNAV_TILE_VARIANT
+#undef MARLNAV_TILE_SET
+
+// rows per lane for a launch: 2 once the RPL=1 grid is several rounds of
+// waves (MARLNAV_RPL=1|2 forces one, for tuning)
+int pick_rpl(int64_t P, int A)
+{
+    static const int forced = [] {
+        const char *v = getenv("MARLNAV_RPL");
+        return v ? (int)strtol(v, nullptr, 10) : 0;
+    }();
+    if (forced == 1 || forced == 2) return forced;
+    const int64_t waves1 = (P + tile_envs(A) - 1) / tile_envs(A);
+    return waves1 >= kRpl2Waves ? 2 : 1;
+}
 
 bool aligned(const void *p, uintptr_t n) { return (reinterpret_cast<uintptr_t>(p) & (n - 1)) == 0; }
 
@@ -1504,6 +1586,7 @@ const TilePair *select_tile(const MarlnavDims *d, const MarlnavStepBuffers &b, b
     for (const TilePair &v : kTileVariants)
         if (v.A == d->num_agents && v.O == d->num_obstacles) t = &v;
     if (!t || tile_envs(t->A) != pick_wave_envs(t->A, t->O, t->O)) return nullptr;
+    if (tile_kernel_envs(t->A, 2) % 4 != 0) return nullptr;
     if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
         !aligned(b.obs, 16))
         return nullptr;
@@ -1513,14 +1596,20 @@ const TilePair *select_tile(const MarlnavDims *d, const MarlnavStepBuffers &b, b
     return t;
 }
 
-int launch_tile(TileFn fn, size_t lds, const Launch &L, const StepArgs &args,
+int launch_tile(TileFn fn, size_t lds, int rpl, const Launch &L, const StepArgs &args,
                 const MarlnavParams &pr, void *stream, const char *what)
 {
     KArgs ka;
     ka.a = args;
     ka.p = pr;
+    // the tile kernels' own tiles (W = tile_kernel_envs(A)); the counter slot
+    // stride stays the wave_kernel count from plan_launch (>= waves here)
+    const int64_t W = tile_kernel_envs(args.A, rpl);
+    ka.a.W = (int)W;
+    ka.a.ntiles = (args.P + W - 1) / W;
+    const int64_t blocks = (ka.a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     void *kargs[] = {&ka};
-    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)L.blocks),
+    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)blocks),
                                    dim3(64 * kWavesPerBlock), kargs, lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
@@ -1612,9 +1701,12 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavSte
     args.b = *b;
     args.step_idx = step_idx;
     const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
-    if (const TilePair *t = select_tile(d, *b, false))
-        return launch_tile(noisy ? t->noisy : t->step, t->lds, L, args, *pr, stream,
+    if (const TilePair *t = select_tile(d, *b, false)) {
+        const int r = pick_rpl(d->num_parallel, d->num_agents);
+        const TileSet &ts = t->rpl[r - 1];
+        return launch_tile(noisy ? ts.noisy : ts.step, ts.lds, r, L, args, *pr, stream,
                            "marlnav_step");
+    }
     const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
     return launch(noisy ? k.noisy : k.step, L, args, *pr, stream, "marlnav_step");
 }
@@ -1634,8 +1726,11 @@ int marlnav_observe(const MarlnavDims *d, const float *states, const float *obst
     MarlnavParams pr;
     memset(&pr, 0, sizeof(pr));
     pr.cap_distance = 0.1f;  // environment.py:65
-    if (const TilePair *t = select_tile(d, args.b, true))
-        return launch_tile(t->obs, t->lds, L, args, pr, stream, "marlnav_observe");
+    if (const TilePair *t = select_tile(d, args.b, true)) {
+        const int r = pick_rpl(d->num_parallel, d->num_agents);
+        return launch_tile(t->rpl[r - 1].obs, t->rpl[r - 1].lds, r, L, args, pr, stream,
+                           "marlnav_observe");
+    }
     return launch(select_kernels(d->num_agents, d->num_obstacles).obs, L, args, pr, stream,
                   "marlnav_observe");
 }

@@ -171,7 +171,8 @@ class _nullctx:
 
 @pytest.mark.parametrize("P,A,O,steps", [(4096, 3, 3, 60), (1000, 3, 8, 40),
                                          (512, 16, 32, 12), (333, 5, 2, 30),
-                                         (65536, 3, 3, 6)])
+                                         (65536, 3, 3, 6), (409600 + 27, 3, 3, 3),
+                                         (2 * 16384 * 32 + 5, 2, 1, 2)])
 def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps):
     """Native (Philox) re-init mode, many steps, random actions, short
     episodes: the GPU trajectory equals the oracle's bit for bit."""
