@@ -1414,9 +1414,442 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
         uint64_t *cnt = kl->a.b.counters;
         const int64_t slots = kl->a.waves;
         if (cnt) {
-            if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + gw], (unsigned long long)c_trunc);
-            if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + gw], (unsigned long long)c_col);
-            if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + gw], (unsigned long long)c_tar);
+            const int64_t sl = gw % slots;  // slots may be fewer than this grid's waves
+            if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
+            if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + sl], (unsigned long long)c_col);
+            if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
+        }
+    }
+#if MARLNAV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(7);
+    if (lane == 0) {
+        g_stamps[(size_t)gw * 24 + 16] = t_entry;
+        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+    }
+#endif
+}
+
+// ------------------------------------------------------ pair-split kernel
+// For shapes whose rows carry many pairs (A16/O32: 48 per row) or grids too
+// small to fill the chip with one lane per row: LPR lanes share each agent
+// row. Lane q of a row evaluates the target pair (kept by q == 0), obstacles
+// q, q+LPR, ... and other agents q, q+LPR, ...; the packed observation rows
+// are assembled in LDS and streamed out with vector stores; per-row flags
+// and counts are OR/sum-reduced across the LPR lanes with DPP / swizzles;
+// the row's bond terms (environment.py:264-269) are evaluated by the lanes
+// that own the distances and summed by the row leader in torch's order.
+template <int A, int O, int LPR>
+struct SplitPlan {
+    static constexpr int EPW = 64 / LPR / A;  // envs per wave
+    static constexpr int R = EPW * A;         // rows per wave
+    static constexpr int D = 2 + 2 * O + 2 * (A - 1);
+    static constexpr int NOB = (O + LPR - 1) / LPR;        // obstacle pairs per lane
+    static constexpr int NAG = (A - 1 + LPR - 1) / LPR;    // other-agent pairs per lane
+    static constexpr int ST = 0;                           // (R, 5)
+    static constexpr int ACT = (ST + R * 5 + 3) & ~3;      // (R, 2)
+    static constexpr int OB = (ACT + R * 2 + 3) & ~3;      // (EPW, O, 2)
+    static constexpr int TG = (OB + EPW * O * 2 + 3) & ~3; // (EPW, 2)
+    static constexpr int SN = (TG + EPW * 2 + 3) & ~3;     // (EPW,)
+    static constexpr int OBS = (SN + EPW + 3) & ~3;        // (R, D)
+    static constexpr int BOND = (OBS + R * D + 3) & ~3;    // (R, A-1)
+    static constexpr int RED = (BOND + R * (A - 1) + 3) & ~3;  // (R, 4)
+    static constexpr int FLOATS = RED + 4 * R;
+    static_assert(EPW >= 1, "an env's rows must fit one wave");
+};
+
+__host__ __device__ constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
+
+// global -> LDS copy of NB bytes whose source is ALIGN-byte aligned: 16-byte
+// LDS-DMA when possible, else dword LDS-DMA (NB % 4 == 0, ALIGN % 4 == 0).
+template <int NB, int ALIGN>
+__device__ __forceinline__ void glds_span_aligned(const void *src, float *dst, unsigned lane)
+{
+    if constexpr (ALIGN % 16 == 0) {
+        glds_span<NB>(src, dst, lane);
+    } else {
+        static_assert(NB % 4 == 0 && ALIGN % 4 == 0, "dword-aligned span");
+        constexpr int N4 = NB / 4;
+#pragma unroll
+        for (int kk = 0; kk * 64 < N4; ++kk) {
+            const char *s = in_sgpr(reinterpret_cast<const char *>(src) + kk * 256);
+            if ((kk + 1) * 64 <= N4 || (int)lane < N4 - kk * 64)
+                __builtin_amdgcn_global_load_lds(s + lane * 4u, (LdsVoid *)(dst + kk * 64), 4, 0, 0);
+        }
+    }
+}
+
+// OR / sum over the LPR consecutive lanes of a row (LPR a power of two)
+template <int LPR>
+__device__ __forceinline__ unsigned lpr_or(unsigned v)
+{
+    if constexpr (LPR >= 2) v |= (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    if constexpr (LPR >= 4) v |= (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    if constexpr (LPR >= 8) v |= (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);
+    if constexpr (LPR >= 16) v |= (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x201F);
+    return v;
+}
+
+template <int LPR>
+__device__ __forceinline__ int lpr_sum(int v)
+{
+    if constexpr (LPR >= 2) v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+    if constexpr (LPR >= 4) v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+    if constexpr (LPR >= 8) v += __builtin_amdgcn_ds_swizzle(v, 0x101F);
+    if constexpr (LPR >= 16) v += __builtin_amdgcn_ds_swizzle(v, 0x201F);
+    return v;
+}
+
+// This lane's pairs of its row: distances and bearings into the LDS row
+// `orow`; with TERMS also the per-lane reward flags and bond terms.
+struct SplitTerms {
+    unsigned fl;  // 1 ob_risk, 2 ob_col, 4 ag_risk, 8 ag_col
+    int band;
+    float ta, td;
+};
+
+template <int A, int O, int LPR, bool TERMS, bool FAST>
+__device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
+                                                  const float *__restrict__ obe,
+                                                  const float *__restrict__ tge, int a, int q,
+                                                  float ox, float oy, float dx, float dy,
+                                                  float *__restrict__ orow,
+                                                  float *__restrict__ bond_row,
+                                                  const MarlnavParams &pr, bool &ok)
+{
+    using SP = SplitPlan<A, O, LPR>;
+    const float cap = pr.cap_distance;
+    SplitTerms t{0u, 0, 0.0f, 0.0f};
+    {
+        const float d = pair_dist(ox, oy, tge[0], tge[1]);
+        const float ang = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, d, cap, ok);
+        t.ta = ang;
+        t.td = d;
+        if (q == 0) {
+            orow[0] = ang;
+            orow[1] = d;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < SP::NOB; ++i) {
+        const int j = q + LPR * i;
+        if (O % LPR == 0 || j < O) {
+            const float px = obe[2 * j], py = obe[2 * j + 1];
+            const float d = pair_dist(ox, oy, px, py);
+            orow[2 + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
+            orow[2 + O + j] = d;
+            if (TERMS)
+                t.fl |= (d < pr.ob_risk_dist ? 1u : 0u) | (d < pr.ob_coll_dist ? 2u : 0u);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < SP::NAG; ++i) {
+        const int kx = q + LPR * i;  // index among the others
+        if ((A - 1) % LPR == 0 || kx < A - 1) {
+            const int m = kx + (kx >= a ? 1 : 0);
+            const float px = sts[5 * m], py = sts[5 * m + 1];
+            const float d = pair_dist(ox, oy, px, py);
+            orow[2 + 2 * O + kx] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
+            orow[2 + 2 * O + (A - 1) + kx] = d;
+            if (TERMS) {
+                t.fl |= (d < pr.ag_risk_dist ? 4u : 0u) | (d < pr.ag_coll_dist ? 8u : 0u);
+                t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
+                const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
+                bond_row[kx] = 1.0f / (1.0f + sd * sd);
+            }
+        }
+    }
+    return t;
+}
+
+template <int A, int O, int LPR, bool OBS_ONLY, bool NOISY>
+__global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
+{
+    using SP = SplitPlan<A, O, LPR>;
+    constexpr int EPW = SP::EPW, R = SP::R, D = SP::D;
+    (void)k;  // read through kargs_late()
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+#if MARLNAV_STAMPS
+    unsigned long long t_entry;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
+#endif
+    const unsigned lane = threadIdx.x & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wib;
+    const int64_t tile = gw;
+    KArgsK *K = kargs_late();
+    const int64_t P = K->a.P;
+    if (tile >= K->a.ntiles) return;
+    STAMP(0);
+    const StepPtrs b = load_ptrs(K);
+    float *wl = lds + wib * SP::FLOATS;
+    float *st = wl + SP::ST;
+    const int64_t e0 = tile * EPW;
+    const int ne = (int)((P - e0) < EPW ? (P - e0) : EPW);
+    const int nr = ne * A;
+
+    // ---- stage the tile (the per-env scalars go straight to the env lanes)
+    if (ne == EPW) {
+        glds_span_aligned<R * 20, gcd_c(R * 20, 16)>(b.states + e0 * (A * 5), st, lane);
+        if (!OBS_ONLY)
+            glds_span_aligned<R * 8, gcd_c(R * 8, 16)>(b.actions + e0 * (A * 2), wl + SP::ACT, lane);
+        glds_span_aligned<EPW * O * 8, gcd_c(EPW * O * 8, 16)>(b.obstacles + e0 * (O * 2),
+                                                              wl + SP::OB, lane);
+        glds_span_aligned<EPW * 8, gcd_c(EPW * 8, 16)>(b.target + e0 * 2, wl + SP::TG, lane);
+    } else {
+        copy_span(b.states + e0 * (A * 5), st, nr * 5, (int)lane);
+        if (!OBS_ONLY) copy_span(b.actions + e0 * (A * 2), wl + SP::ACT, nr * 2, (int)lane);
+        copy_span(b.obstacles + e0 * (O * 2), wl + SP::OB, ne * O * 2, (int)lane);
+        copy_span(b.target + e0 * 2, wl + SP::TG, ne * 2, (int)lane);
+    }
+    const bool env_on = (int)lane < ne;
+    float sn_in = 0.0f;
+    unsigned term_in = 0u;
+    if (!OBS_ONLY && env_on) {
+        sn_in = b.step_num[e0 + lane];
+        term_in = b.terminates[e0 + lane];
+    }
+    const MarlnavParams pr = load_params(K);
+    const int row = (int)lane / LPR, q = (int)lane - row * LPR;
+    const int rowc = row < R ? row : 0;  // idle lanes shadow row 0 (results unused)
+    const int el = rowc / A, a = rowc - el * A;
+    const bool row_on = row < nr;
+    unsigned c_trunc = 0, c_col = 0, c_tar = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
+    wave_sync();
+    STAMP(1);
+
+    // ---- _move_agents (environment.py:113-123): every lane of a row moves
+    // it (same instructions either way), the row leader stores it
+    float ox = st[5 * rowc], oy = st[5 * rowc + 1];
+    float dx = st[5 * rowc + 2], dy = st[5 * rowc + 3];
+    if (!OBS_ONLY) {
+        const float2 act = reinterpret_cast<const float2 *>(wl + SP::ACT)[rowc];
+        float a0 = act.x, a1 = act.y;
+        if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
+            KArgsK *kl = kargs_late();
+            a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
+            a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
+        }
+        float sn, c;
+        sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+        const float ndx = c * dx + (-sn) * dy;
+        const float ndy = sn * dx + c * dy;
+        const float v = clamp_t(st[5 * rowc + 4] + clamp_t(a1, pr.min_accel, pr.max_accel),
+                                pr.min_speed, pr.max_speed);
+        ox = ox + ndx * v;
+        oy = oy + ndy * v;
+        dx = ndx;
+        dy = ndy;
+        wave_sync();  // every lane has read the pre-move rows
+        if (row_on && q == 0) {
+            float *s = st + 5 * row;
+            s[0] = ox;
+            s[1] = oy;
+            s[2] = dx;
+            s[3] = dy;
+            s[4] = v;
+        }
+        wave_sync();
+    }
+    STAMP(2);
+
+    // ---- observations + per-lane reward terms (:99-100)
+    const float *sts = st + 5 * A * el;
+    const float *obe = wl + SP::OB + 2 * O * el;
+    const float *tge = wl + SP::TG + 2 * el;
+    float *orow = wl + SP::OBS + rowc * D;
+    float *brow = wl + SP::BOND + rowc * (A - 1);
+    {
+        bool ok = true;
+        SplitTerms t = split_pairs<A, O, LPR, !OBS_ONLY, true>(sts, obe, tge, a, q, ox, oy, dx, dy,
+                                                             orow, brow, pr, ok);
+        ok = ok || !row_on;
+        if (__builtin_expect(__ballot(!ok) != 0ull, 0)) {  // IEEE redo, rare
+            ok = true;
+            t = split_pairs<A, O, LPR, !OBS_ONLY, false>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
+                                                        brow, pr, ok);
+        }
+        if (!OBS_ONLY) {
+            const unsigned fl = lpr_or<LPR>(t.fl);
+            const int band = lpr_sum<LPR>(t.band);
+            wave_sync();  // bond terms of the row are in LDS
+            if (row_on && q == 0) {
+                const float head = fabsf(t.ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+                const float bandf = (float)band;
+                const float dsc = (bandf < pr.max_at_prop_d ? bandf : pr.max_at_prop_d) / pr.max_at_prop_d;
+                const float soft = -1.0f * (t.td / pr.init_dist);
+                float bv[A - 1];
+#pragma unroll
+                for (int i = 0; i < A - 1; ++i) bv[i] = brow[i];
+                const float bond = torch_row_sum_r<A - 1>(bv, [](float x) { return x; });
+                const float bondm = bond / (float)(A - 1);
+                const float risk = (fl & 5u) ? 1.0f : 0.0f;
+                float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
+                float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
+                rm = rm + pr.distance_factor * dsc;
+                rh = rh + pr.distance_factor * dsc;
+                rm = rm + pr.soft_factor * soft;
+                rh = rh + pr.soft_factor * soft;
+                rm = rm + pr.bond_factor * bondm;
+                rh = rh + pr.bond_factor * bondm;
+                rm = rm - pr.risk_factor * risk;
+                rh = rh - pr.risk_factor * risk;
+                const unsigned flags = ((fl & 10u) ? 1u : 0u) | ((t.td < pr.target_radius) ? 2u : 0u);
+                reinterpret_cast<float4 *>(wl + SP::RED)[row] =
+                    make_float4(rm, rh, __uint_as_float(flags), 0.0f);
+            }
+        }
+    }
+    STAMP(3);
+
+    if (!OBS_ONLY) {
+        wave_sync();
+        // ---- per-env reductions, terminal logic, masked re-init
+        bool fin = false, tr_l = false, co_l = false, ta_l = false;
+        if (env_on) {
+            const int64_t e = e0 + lane;
+            const float4 *red = reinterpret_cast<const float4 *>(wl + SP::RED) + A * lane;
+            unsigned any_col = 0u, all_in = 1u;
+            float rm[A], rh[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i) {
+                const float4 r = red[i];
+                const unsigned f = __float_as_uint(r.z);
+                any_col |= f & 1u;
+                all_in &= (f >> 1) & 1u;
+                rm[i] = r.x;
+                rh[i] = r.y;
+            }
+            float rv[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
+            const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
+            b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
+            float step_num = sn_in + 1.0f;                     // :96
+            const bool truncated = step_num > pr.trunc_after;  // :97
+            const bool term_old = term_in != 0u;
+            const bool terminated = any_col || term_old;       // :213-214
+            b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
+            b.terminated[e] = (uint8_t)terminated;
+            b.truncated[e] = (uint8_t)truncated;
+            fin = truncated || terminated;                     // :102-104
+            if (fin) {
+                KArgsK *kl = kargs_late();
+                MarlnavParams p;  // the fields the re-init reads
+                p.obs_range_x = kl->p.obs_range_x;
+                p.obs_mean_x = kl->p.obs_mean_x;
+                p.obs_range_y = kl->p.obs_range_y;
+                p.obs_mean_y = kl->p.obs_mean_y;
+                p.ags_dist = kl->p.ags_dist;
+                p.noise_std = kl->p.noise_std;
+                p.angle_range = kl->p.angle_range;
+                p.flags = kl->p.flags;
+                p.seed = kl->p.seed;
+                float *s5 = st + 5 * A * lane;
+                float *obl = wl + SP::OB + 2 * O * lane;
+                float *tgl = wl + SP::TG + 2 * lane;
+                const float *fs = kl->a.b.fresh_states;
+                float *gob = kl->a.b.obstacles;
+                float *gtg = kl->a.b.target;
+                if (fs) {
+                    const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
+                    if (!(p.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
+                        for (int i = 0; i < 5 * A; ++i) s5[i] = fs[e * A * 5 + i];
+                    for (int i = 0; i < 2 * O; ++i) obl[i] = fo[e * O * 2 + i];
+                    tgl[0] = ft[2 * e];
+                    tgl[1] = ft[2 * e + 1];
+                } else {
+                    native_fresh_env<NOISY>(A, O, p, kl->a.b.formation,
+                                            (uint64_t)(kl->a.env_offset + e), kl->a.step_idx, s5,
+                                            obl, tgl);
+                }
+                for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
+                gtg[2 * e] = tgl[0];
+                gtg[2 * e + 1] = tgl[1];
+                step_num = 0.0f;
+            }
+            b.step_num[e] = step_num;
+            tr_l = truncated;
+            co_l = any_col;
+            ta_l = all_in;
+        }
+        const uint64_t finmask = __ballot(fin);
+        c_trunc = __popcll(__ballot(tr_l));
+        c_col = __popcll(__ballot(co_l));
+        c_tar = __popcll(__ballot(ta_l));
+        STAMP(4);
+
+        // ---- observations of re-initialised envs (:105)
+        if (finmask) {
+            wave_sync();
+            const bool redo = row_on && ((finmask >> el) & 1u);
+            const float *s = st + 5 * rowc;
+            const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
+            bool ok = true;
+            if (redo)
+                split_pairs<A, O, LPR, false, true>(sts, obe, tge, a, q, rx, ry, rdx, rdy, orow,
+                                                   brow, pr, ok);
+            ok = ok || !redo;
+            if (__ballot(!ok) != 0ull && redo)
+                split_pairs<A, O, LPR, false, false>(sts, obe, tge, a, q, rx, ry, rdx, rdy, orow,
+                                                    brow, pr, ok);
+        }
+    }
+    STAMP(5);
+
+    // ---- stream the tile out (obs rows and states from LDS)
+    wave_sync();
+    {
+        const float *src = wl + SP::OBS;
+        float *gobs = in_sgpr(b.obs + e0 * (A * D));
+        const int n = nr * D;
+        constexpr int VAL = gcd_c(R * D * 4, 16);  // tile base alignment in bytes
+        float *gnorm = nullptr;
+        const float *mean = nullptr, *scale = nullptr;
+        if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
+            KArgsK *kl = kargs_late();
+            gnorm = kl->a.b.obs_norm + e0 * (A * D);
+            mean = kl->a.b.norm_mean;
+            scale = kl->a.b.norm_scale;
+        }
+        if (VAL % 16 == 0 && ne == EPW) {
+            for (int i = (int)lane; i < n / 4; i += 64)
+                reinterpret_cast<float4 *>(gobs)[i] = reinterpret_cast<const float4 *>(src)[i];
+        } else if (VAL % 8 == 0 && n % 2 == 0) {
+            for (int i = (int)lane; i < n / 2; i += 64)
+                reinterpret_cast<float2 *>(gobs)[i] = reinterpret_cast<const float2 *>(src)[i];
+        } else {
+            for (int i = (int)lane; i < n; i += 64) gobs[i] = src[i];
+        }
+        if (gnorm)
+            for (int i = (int)lane; i < n; i += 64) {
+                const int kk = i % D;
+                gnorm[i] = (src[i] - mean[kk]) / scale[kk];
+            }
+    }
+    if (!OBS_ONLY) {
+        float *gst = in_sgpr(b.states + e0 * (A * 5));
+        const int n = nr * 5;
+        constexpr int SAL = gcd_c(R * 20, 16);
+        if (SAL % 16 == 0 && ne == EPW) {
+            for (int i = (int)lane; i < n / 4; i += 64)
+                reinterpret_cast<float4 *>(gst)[i] = reinterpret_cast<const float4 *>(st)[i];
+        } else {
+            for (int i = (int)lane; i < n; i += 64) gst[i] = st[i];
+        }
+    }
+    STAMP(6);
+    if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
+        KArgsK *kl = kargs_late();
+        uint64_t *cnt = kl->a.b.counters;
+        const int64_t slots = kl->a.waves;
+        if (cnt) {
+            const int64_t sl = gw % slots;  // slots may be fewer than this grid's waves
+            if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
+            if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + sl], (unsigned long long)c_col);
+            if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
         }
     }
 #if MARLNAV_STAMPS
@@ -1596,6 +2029,69 @@ const TilePair *select_tile(const MarlnavDims *d, const MarlnavStepBuffers &b, b
     return t;
 }
 
+// pair-split kernels (split_kernel): rows with many pairs, or grids too small
+// for one lane per row to fill the chip
+struct SplitVariant {
+    int A, O, epw;
+    TileFn step, obs, noisy;
+    size_t lds;
+    bool always;  // also for large grids
+};
+
+#define MARLNAV_SPLIT_VARIANT(A, O, LPR, ALWAYS)                                          \
+    {A, O, SplitPlan<A, O, LPR>::EPW, split_kernel<A, O, LPR, false, false>,             \
+     split_kernel<A, O, LPR, true, false>, split_kernel<A, O, LPR, false, true>,         \
+     (size_t)SplitPlan<A, O, LPR>::FLOATS * 4 * kWavesPerBlock, ALWAYS}
+const SplitVariant kSplitVariants[] = {
+    MARLNAV_SPLIT_VARIANT(16, 32, 4, true),
+    MARLNAV_SPLIT_VARIANT(3, 8, 4, false),
+    MARLNAV_SPLIT_VARIANT(3, 3, 4, false),
+};
+#undef MARLNAV_SPLIT_VARIANT
+
+// one-lane-per-row grids below kSplitBelowWaves * (pairs per row / 6) waves
+// leave most SIMDs idle (measured: 4096x3x3 and 16384x3x8 split faster,
+// 16384x3x3 does not)
+constexpr int64_t kSplitBelowWaves = 512;
+
+const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only)
+{
+    static const int forced = [] {
+        const char *v = getenv("MARLNAV_SPLIT");
+        return v ? (int)strtol(v, nullptr, 10) : -1;
+    }();
+    if (forced == 0 || d->obstacle_stride != d->num_obstacles) return nullptr;
+    const SplitVariant *v = nullptr;
+    for (const SplitVariant &x : kSplitVariants)
+        if (x.A == d->num_agents && x.O == d->num_obstacles) v = &x;
+    if (!v) return nullptr;
+    const int64_t row_waves = (d->num_parallel + tile_envs(v->A) - 1) / tile_envs(v->A);
+    const int64_t pairs = 1 + v->O + (v->A - 1);
+    if (!v->always && forced != 1 && row_waves * 6 >= kSplitBelowWaves * pairs) return nullptr;
+    if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
+        !aligned(b.obs, 16))
+        return nullptr;
+    if (!obs_only && !aligned(b.actions, 16)) return nullptr;
+    return v;
+}
+
+int launch_split(const SplitVariant &v, TileFn fn, const StepArgs &args, const MarlnavParams &pr,
+                 void *stream, const char *what)
+{
+    KArgs ka;
+    ka.a = args;
+    ka.p = pr;
+    ka.a.W = v.epw;
+    ka.a.ntiles = (args.P + v.epw - 1) / v.epw;
+    const int64_t blocks = (ka.a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    void *kargs[] = {&ka};
+    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)blocks),
+                                   dim3(64 * kWavesPerBlock), kargs, v.lds, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+    return 0;
+}
+
 int launch_tile(TileFn fn, size_t lds, int rpl, const Launch &L, const StepArgs &args,
                 const MarlnavParams &pr, void *stream, const char *what)
 {
@@ -1701,6 +2197,8 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavSte
     args.b = *b;
     args.step_idx = step_idx;
     const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
+    if (const SplitVariant *v = select_split(d, *b, false))
+        return launch_split(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
     if (const TilePair *t = select_tile(d, *b, false)) {
         const int r = pick_rpl(d->num_parallel, d->num_agents);
         const TileSet &ts = t->rpl[r - 1];
@@ -1726,6 +2224,8 @@ int marlnav_observe(const MarlnavDims *d, const float *states, const float *obst
     MarlnavParams pr;
     memset(&pr, 0, sizeof(pr));
     pr.cap_distance = 0.1f;  // environment.py:65
+    if (const SplitVariant *v = select_split(d, args.b, true))
+        return launch_split(*v, v->obs, args, pr, stream, "marlnav_observe");
     if (const TilePair *t = select_tile(d, args.b, true)) {
         const int r = pick_rpl(d->num_parallel, d->num_agents);
         return launch_tile(t->rpl[r - 1].obs, t->rpl[r - 1].lds, r, L, args, pr, stream,
