@@ -153,6 +153,20 @@ int64_t marlnav_counter_slots(const MarlnavDims *dims);
 int marlnav_counters_total(const MarlnavDims *dims, const uint64_t *counters,
                            uint64_t *out3, void *stream);
 
+/* MAPPO._process_rewards (models.py:131-148) on the device. Discounted
+ * returns of a rollout of T steps, G_t = done_t ? 0 : r_t + gamma * G_{t+1}
+ * (G_T = 0), in float64 like the reference (its accumulator is
+ * torch.zeros(P, dtype=float), models.py:133), then normalized in place,
+ * returns = (G - mean) / (std + 1e-12) with the unbiased std over all T*P
+ * values (torch.std_mean, models.py:140-144).
+ *   rewards (T, P) fp32, done (T, P) uint8 (bool), returns (T, P) fp64 out,
+ *   stats: 2 fp64 out (mean, std), work: marlnav_returns_work_size(P) fp64.
+ * All device pointers; enqueued on stream. */
+int64_t marlnav_returns_work_size(int64_t num_parallel);
+int marlnav_discounted_returns(const float *rewards, const uint8_t *done, int64_t T,
+                               int64_t P, double gamma, double *returns, double *stats,
+                               double *work, void *stream);
+
 /* Message of the last failing call on this thread. */
 const char *marlnav_last_error(void);
 

@@ -6,7 +6,7 @@ The package directory is ``marl-nav_amd/``; import it as ``marlnav_amd``
 (the alias module at the repository root) or with
 ``importlib.import_module('marl-nav_amd')``.
 """
-from . import abi, shard
+from . import abi, rollout, shard
 from .environment import Env
 from .utils import (ActionScaler, ConstantSampler, MockInitializer, MockSampler,
                     ObsNormalizer, Observations, TriangleIntitializer, action_sampler, default_args,
@@ -17,4 +17,4 @@ __all__ = ["Env", "Observations", "ObsNormalizer", "ActionScaler", "MockInitiali
            "TriangleIntitializer", "ConstantSampler", "MockSampler", "init_sampler",
            "action_sampler", "set_all_seeds", "set_env_params", "set_init_params",
            "set_sampler_params", "set_normalizer_params", "set_scaler_params", "default_args",
-           "abi", "shard"]
+           "abi", "rollout", "shard"]

@@ -62,6 +62,7 @@ class MarlnavStepBuffers(ctypes.Structure):
 
 EXPORTS = ("marlnav_step", "marlnav_observe", "marlnav_reinit_all",
            "marlnav_counter_slots", "marlnav_counters_total",
+           "marlnav_returns_work_size", "marlnav_discounted_returns",
            "marlnav_last_error", "marlnav_abi_version")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -83,6 +84,11 @@ def _declare(lib):
     lib.marlnav_counter_slots.restype = c.c_int64
     lib.marlnav_counters_total.argtypes = [dims_p, _P, _P, _P]
     lib.marlnav_counters_total.restype = c.c_int
+    lib.marlnav_returns_work_size.argtypes = [c.c_int64]
+    lib.marlnav_returns_work_size.restype = c.c_int64
+    lib.marlnav_discounted_returns.argtypes = [_P, _P, c.c_int64, c.c_int64, c.c_double,
+                                               _P, _P, _P, _P]
+    lib.marlnav_discounted_returns.restype = c.c_int
     lib.marlnav_last_error.argtypes = []
     lib.marlnav_last_error.restype = c.c_char_p
     lib.marlnav_abi_version.argtypes = []

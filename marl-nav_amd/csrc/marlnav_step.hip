@@ -83,6 +83,15 @@ int fail(int code, const char *fmt, ...)
     va_end(ap);
     return code;
 }
+}  // namespace
+
+// error reporting shared with the other translation units of the library
+__attribute__((visibility("hidden"))) int marlnav_internal_fail(int code, const char *msg)
+{
+    return fail(code, "%s", msg);
+}
+
+namespace {
 
 __host__ __device__ inline int obs_dim(int A, int O) { return 2 + 2 * O + 2 * (A - 1); }
 

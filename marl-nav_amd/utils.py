@@ -364,3 +364,111 @@ def set_all_seeds(seed):
         torch.cuda.manual_seed_all(seed)
         torch.backends.cudnn.deterministic = True
         torch.backends.cudnn.benchmark = False
+
+
+def set_animation_params(args, device):
+    """utils.py:194-214 (the keys the reward check reads: max_step,
+    parallel_index, agent_index; the rest kept for callers that pass the
+    dict on)."""
+    return {
+        'size_x': args.fig_size_x, 'size_y': args.fig_size_y,
+        'x_max': args.max_x_value, 'y_max': args.max_y_value,
+        'num_agents': args.num_agents, 'action_size': 2,
+        'parallel_index': args.parallel_index, 'agent_index': args.agent_index,
+        'sampling_style': args.sampling_style, 'random': args.random,
+        'weights_file': args.weights_file, 'max_step': args.max_step,
+        'interval': args.interval,
+        'normalizer': set_normalizer_params(args, device),
+        'scaler': set_scaler_params(args, device),
+    }
+
+
+CHECK_REWS_SERIES = ("target_angles", "target_distances", "all_obs_angels",
+                     "all_obs_distances", "angles_to_first", "distances_to_first",
+                     "angles_to_second", "distances_to_second", "rewards")
+
+
+def check_rews(env, num_steps, parallel_ind, agent_ind, plot_dir='plots', plot=True):
+    """utils.py:579-666: drive ``env`` with its own action sampler for
+    ``num_steps`` steps and record, for env ``parallel_ind`` and agent
+    ``agent_ind``, the nine series the reference plots (angle/distance to the
+    target, to obstacle 0, to the first and second other agent, and the env
+    reward). The series are gathered on the device and read back once (the
+    reference syncs nine times per step). Saves the reference's two figures
+    under ``plot_dir`` when ``plot`` (and matplotlib is importable). Returns
+    {series name: list of floats} (names as in the reference, typos kept)."""
+    A = env.num_agents
+    others = [k for k in range(A) if k != agent_ind]
+    dev = env.device
+    rec = torch.empty(num_steps, 9, device=dev)
+    cols = None
+    for i in range(num_steps):
+        actions = env.sample_actions()
+        obs, rew, _, _ = env.step(actions)
+        packed = getattr(obs, '_packed', None)
+        if packed is None:
+            packed = torch.cat(tuple(obs), dim=2)
+        if cols is None:
+            # observed obstacles: the obs width, which can be below
+            # num_obstacles (environment.py:148-152, mock scenarios)
+            O, D = obs[2].shape[-1], packed.shape[-1]
+            nsec = 1 if len(others) > 1 else 0
+            packed_cols = [0, 1, 2, 2 + O, 2 + 2 * O, 2 + 2 * O + (A - 1),
+                           2 + 2 * O + nsec, 2 + 2 * O + (A - 1) + nsec]
+            if max(packed_cols) >= D or not (0 <= parallel_ind < packed.shape[0]
+                                             and 0 <= agent_ind < A):
+                raise IndexError(f"check_rews: index out of range for obs {tuple(packed.shape)}")
+            cols = torch.tensor(packed_cols, device=dev)
+        rec[i, :8] = packed[parallel_ind, agent_ind].index_select(0, cols)
+        rec[i, 8] = rew[parallel_ind]
+    vals = rec.cpu().tolist()
+    series = {name: [row[k] for row in vals] for k, name in enumerate(CHECK_REWS_SERIES)}
+    if plot:
+        _plot_check_rews(env, series, parallel_ind, agent_ind, others, plot_dir)
+    return series
+
+
+def _plot_check_rews(env, series, parallel_ind, agent_ind, others, plot_dir):
+    """The two figures of utils.py:614-666, same titles and file names."""
+    import os
+    try:
+        import matplotlib
+        matplotlib.use('Agg')
+        import matplotlib.pyplot as plt
+    except ImportError:
+        return
+    first, second = others[0], others[1 if len(others) > 1 else 0]
+    pi_plus = 3.5
+    fig, axs = plt.subplots(4, 2, figsize=(10, 10))
+    panels = [("target_angles", 'Angle to target (rad)', True),
+              ("target_distances", 'Distance to target', False),
+              ("all_obs_angels", 'Angle to obstacle (rad)', True),
+              ("all_obs_distances", 'Distance to obstacle', False),
+              ("angles_to_first", 'Angle to agent {} (rad)'.format(first), True),
+              ("distances_to_first", 'Distance to agent {}'.format(first), False),
+              ("angles_to_second", 'Angle to agent {} (rad)'.format(second), True),
+              ("distances_to_second", 'Distance to agent {}'.format(second), False)]
+    for ax, (key, title, is_angle) in zip(axs.flat, panels):
+        ax.plot(series[key])
+        ax.set_title(title)
+        if is_angle:
+            ax.set_ylim([-pi_plus, pi_plus])
+    fig.tight_layout(pad=5.0)
+    for ax in axs.flat:
+        ax.set(xlabel='step number', ylabel='value')
+    fig.suptitle('States, parallel index: {0}, agent index: {1}'.format(parallel_ind, agent_ind))
+    os.makedirs(plot_dir, exist_ok=True)
+    fig.savefig(os.path.join(plot_dir, 'states_array_{0}_agent_{1}.png'.format(
+        parallel_ind, agent_ind)))
+    plt.close(fig)
+    fac = (env._target_factor, env._heading_factor, env._distance_factor, env._risk_factor,
+           env._soft_factor, env._bond_factor)
+    fig, ax = plt.subplots(1, 1)
+    ax.set(xlabel='step number', ylabel='value')
+    ax.plot(series["rewards"])
+    fig.suptitle('Rewards, parallel index: {0}, agent index: {1}'.format(parallel_ind, agent_ind)
+                 + '\n Factors: tar {0}, hea {1}'.format(fac[0], fac[1])
+                 + ', dis {0}, ris {1}, sof {2} bof {3}'.format(fac[2], fac[3], fac[4], fac[5]))
+    fig.savefig(os.path.join(plot_dir, 'rewards_B{0}A{1}T{2}H{3}D{4}R{5}S{6}.png'.format(
+        parallel_ind, agent_ind, *fac[:5], fac[5])))
+    plt.close(fig)

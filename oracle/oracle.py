@@ -46,6 +46,9 @@ def load():
         lib.oracle_normalize.restype = None
         lib.oracle_sincos.argtypes = [ctypes.c_float, P, P]
         lib.oracle_sincos.restype = None
+        lib.oracle_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P,
+                                                  ctypes.c_double, P, P]
+        lib.oracle_discounted_returns.restype = None
         _lib = lib
     return _lib
 
@@ -160,3 +163,16 @@ def split_obs(obs, A, O):
     sizes = [1, 1, O, O, A - 1, A - 1]
     edges = np.cumsum([0] + sizes)
     return [obs[..., edges[i]:edges[i + 1]] for i in range(6)]
+
+
+def discounted_returns(rewards, done, gamma):
+    """MAPPO._process_rewards (models.py:131-148) on (T, P) arrays: returns the
+    normalized float64 returns (T, P) and (mean, std)."""
+    rew = _f32(rewards)
+    dn = np.ascontiguousarray(np.asarray(done, np.bool_)).view(np.uint8)
+    T, P = rew.shape
+    out = np.empty((T, P), np.float64)
+    stats = np.empty(2, np.float64)
+    load().oracle_discounted_returns(T, P, _ptr(rew), _ptr(dn), float(gamma), _ptr(out),
+                                     _ptr(stats))
+    return out, (float(stats[0]), float(stats[1]))

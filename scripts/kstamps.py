@@ -25,7 +25,7 @@ def main():
         env = pkg.Env(params)
         lib = env._lib
         lib.marlnav_debug_stamps.argtypes = [ctypes.c_void_p]
-        nb = env._counters.shape[1]
+        nb = P + 64  # >= waves of any step kernel (one env per wave at most)
         buf = torch.zeros(nb * 24, dtype=torch.int64, device="cuda")
         assert lib.marlnav_debug_stamps(buf.data_ptr()) == 0
         acts = torch.zeros(P, A, 2, device="cuda")

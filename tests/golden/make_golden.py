@@ -21,6 +21,9 @@ Fixture classes:
   scenarios ``-sn 0`` / ``-sn 1`` (utils.py:35-115, 419-451).
 * F4 ``triangle_rng.npz`` - successive draws of ``TriangleIntitializer``
   after ``set_all_seeds`` (utils.py:375-398, 550-559).
+* F5 ``process_rewards.npz`` - ``MAPPO._process_rewards`` (models.py:131-148)
+  run unmodified (as an unbound method on a stand-in holding only the
+  attributes it reads) over seeded reward/done rollouts.
 
 Run:  PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py
 """
@@ -235,7 +238,38 @@ def make_triangle_rng(seeds=(0, 1, 7), P=8, O=3, draws=4):
     return "triangle_rng", rec, meta
 
 
+# ------------------------------------------------------- F5 process_rewards
+class _RolloutHolder(object):
+    """The attributes MAPPO._process_rewards reads and writes."""
+
+
+def make_process_rewards(cases=((24, 96, 0.9, 21, 0.1), (7, 5, 0.99, 22, 0.3),
+                                (1, 33, 0.9, 23, 0.0))):
+    from marlnav.models import MAPPO
+    rec, meta = {}, {"kind": "F5", "cases": []}
+    for k, (T, P, gamma, seed, p_done) in enumerate(cases):
+        g = torch.Generator().manual_seed(seed)
+        rew = (torch.randn(T, P, generator=g) * 200.0).to(torch.float32)
+        done = torch.rand(T, P, generator=g) < p_done
+        h = _RolloutHolder()
+        h.buffer = [[None, None, None, None, rew[t].clone(), done[t].clone()] for t in range(T)]
+        h.buffer_len, h.num_parallel, h.device, h.gamma = T, P, "cpu", gamma
+        h._logs = {"mean_rews": []}
+        h._mean_rew = 0.0
+        MAPPO._process_rewards(h)
+        rec[f"case{k}_rewards"] = rew.numpy()
+        rec[f"case{k}_done"] = done.numpy()
+        rec[f"case{k}_returns"] = np.stack([h.buffer[t][-2].numpy() for t in range(T)])
+        rec[f"case{k}_mean"] = np.float64(h._mean_rew.item())
+        meta["cases"].append({"T": T, "P": P, "gamma": gamma, "seed": seed, "p_done": p_done,
+                              "returns_dtype": str(h.buffer[0][-2].dtype)})
+    return "process_rewards", rec, meta
+
+
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", help="fixture names to (re)generate")
+    cli = ap.parse_args()
     torch.set_num_threads(1)
     all_factors = dict(risk_factor=3., distance_factor=7., heading_factor=500.,
                        target_factor=500., soft_factor=500., bond_factor=10.)
@@ -249,18 +283,26 @@ def main():
         make_trace("trace_mock0", 0, 1000, None),
         make_trace("trace_mock1", 1, 1000, None),
         make_triangle_rng(),
-    ]
+        make_process_rewards(),
+    ] if not cli.only else [JOBS[n]() for n in cli.only]
+    mpath = os.path.join(HERE, "MANIFEST.json")
     manifest = {"torch": torch.__version__, "numpy": np.__version__,
                 "cpu_capability": torch.backends.cpu.get_cpu_capability(),
                 "reference": "JussiM01/MARL-nav @ 2025-10-03 (imported unmodified)",
                 "generator": "tests/golden/make_golden.py", "files": {}}
+    if cli.only and os.path.exists(mpath):
+        with open(mpath) as fh:
+            manifest["files"] = json.load(fh)["files"]
     for name, arrays, meta in jobs:
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **arrays)
         manifest["files"][name + ".npz"] = meta
         print(f"{name}: {os.path.getsize(path)} bytes")
-    with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
+    with open(mpath, "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)
+
+
+JOBS = {"process_rewards": make_process_rewards, "triangle_rng": make_triangle_rng}
 
 
 if __name__ == "__main__":

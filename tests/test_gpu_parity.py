@@ -1,11 +1,13 @@
 """Parity of the HIP step (libmarlnav.so through the drop-in Env) with the
 reference's golden vectors and with the C oracle. Needs an MI355X."""
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import (OBS_FIELDS, assert_obs_close, assert_states_close, assert_vec_close,
-                      cli_args, env_values, golden, meta)
+from conftest import (ANGLE_ATOL, OBS_FIELDS, ROOT, RTOL, assert_obs_close,
+                      assert_states_close, assert_vec_close, cli_args, env_values, golden, meta)
 
 import oracle as orc
 
@@ -336,3 +338,104 @@ def test_step_outputs_never_alias_live_tensors(pkg):
         ptrs.add(o._packed.data_ptr())
         del o, r, te, tr
     assert len(ptrs) <= 4
+
+
+def test_discounted_returns_match_reference_and_oracle(pkg):
+    """§8(f) row 3: the device scan against MAPPO._process_rewards run
+    unmodified (F5) and the C oracle at rollout size; float64 within 1e-12."""
+    from conftest import golden, meta
+    z = golden("process_rewards")
+    for k, m in enumerate(meta("process_rewards")["cases"]):
+        rew = torch.from_numpy(z[f"case{k}_rewards"]).to(DEV)
+        done = torch.from_numpy(z[f"case{k}_done"]).to(DEV)
+        ret, mean, std = pkg.rollout.discounted_returns(rew, done, m["gamma"])
+        np.testing.assert_allclose(np_(ret), z[f"case{k}_returns"], rtol=1e-12, atol=1e-12)
+        assert abs(mean.item() - float(z[f"case{k}_mean"])) <= 1e-12 * max(1., abs(mean.item()))
+    g = torch.Generator().manual_seed(3)
+    T, P = 64, 65536 + 17
+    rew = torch.randn(T, P, generator=g) * 50
+    done = torch.rand(T, P, generator=g) < 0.02
+    ret, mean, std = pkg.rollout.discounted_returns(rew.to(DEV), done.to(DEV), 0.97)
+    oret, (omean, ostd) = orc.discounted_returns(rew.numpy(), done.numpy(), 0.97)
+    np.testing.assert_allclose(np_(ret), oret, rtol=1e-10, atol=1e-10)
+    assert abs(mean.item() - omean) <= 1e-12 * abs(omean) and abs(std.item() - ostd) <= 1e-12 * ostd
+
+
+def test_process_rewards_list_buffer_and_rollout_buffer(pkg):
+    """The list-buffer drop-in updates entries like models.py:134-144; the
+    stacked RolloutBuffer gives the same returns."""
+    from conftest import golden, meta
+    z = golden("process_rewards")
+    m = meta("process_rewards")["cases"][0]
+    rew = torch.from_numpy(z["case0_rewards"]).to(DEV)
+    done = torch.from_numpy(z["case0_done"]).to(DEV)
+    T, P = rew.shape
+    obs = torch.zeros(P, 3, 12, device=DEV)
+    buf = [[obs, None, None, None, rew[t].clone(), done[t].clone()] for t in range(T)]
+    mean = pkg.rollout.process_rewards(buf, m["gamma"])
+    assert buf[0][0] is obs and buf[0][-2].dtype == torch.float64
+    np.testing.assert_allclose(np.stack([np_(e[-2]) for e in buf]), z["case0_returns"],
+                               rtol=1e-12, atol=1e-12)
+    rb = pkg.rollout.RolloutBuffer(T)
+    for t in range(T):
+        rb.add(obs, torch.zeros(P * 3, 2, device=DEV), torch.zeros(P * 3, device=DEV),
+               torch.zeros(P, 1, device=DEV), rew[t], done[t])
+    mean2 = rb.process_rewards(m["gamma"])
+    assert mean2.item() == mean.item()
+    ents = rb.entries()
+    assert len(ents) == T and ents[3][4].dtype == torch.float64
+    np.testing.assert_array_equal(np.stack([np_(e[4]) for e in ents]),
+                                  np.stack([np_(e[-2]) for e in buf]))
+
+
+def _check_rews_expected(z, steps, p, a, A=3, O=3):
+    """The nine check_rews series (utils.py:595-613) read off a trace fixture."""
+    return {
+        "target_angles": z["obs_target_angle"][:steps, p, a, 0],
+        "target_distances": z["obs_target_distance"][:steps, p, a, 0],
+        "all_obs_angels": z["obs_obstacles_angles"][:steps, p, a, 0],
+        "all_obs_distances": z["obs_obstacles_distances"][:steps, p, a, 0],
+        "angles_to_first": z["obs_others_angles"][:steps, p, a, 0],
+        "distances_to_first": z["obs_others_distances"][:steps, p, a, 0],
+        "angles_to_second": z["obs_others_angles"][:steps, p, a, 1],
+        "distances_to_second": z["obs_others_distances"][:steps, p, a, 1],
+        "rewards": z["reward"][:steps, p],
+    }
+
+
+@pytest.mark.parametrize("name,agent", [("trace_cfg1", 0), ("trace_mock1", 2)])
+def test_check_rews_series_match_reference(pkg, name, agent, tmp_path):
+    """§8(f) row 4: check_rews (utils.py:579-666) records the reference's nine
+    series (F2/F3 traces) and writes its two figures."""
+    m, env = _trace_env(pkg, name)
+    z = golden(name)
+    steps = 300
+    series = pkg.utils.check_rews(env, steps, 1, agent, plot_dir=str(tmp_path), plot=True)
+    exp = _check_rews_expected(z, steps, 1, agent, O=z["obs_obstacles_angles"].shape[-1])
+    assert list(series) == list(pkg.utils.CHECK_REWS_SERIES)
+    for k, v in exp.items():
+        atol = ANGLE_ATOL if "angle" in k or "angels" in k else 0.0
+        np.testing.assert_allclose(np.asarray(series[k]), v, rtol=RTOL, atol=atol, err_msg=k)
+    names = sorted(os.listdir(tmp_path))
+    assert f"states_array_1_agent_{agent}.png" in names and any(n.startswith("rewards_B1") for n in names)
+
+
+def test_cli_reward_check_matches_reference(pkg):
+    """``python -m marlnav_amd -rc -se 0 --init-noise-device cpu`` prints the
+    reference's CPU config-1 series (F2) - the plumbing run of BASELINE
+    configs[0]."""
+    import subprocess
+    import sys
+    steps = 120
+    out = subprocess.run([sys.executable, "-m", "marlnav_amd", "-rc", "-se", "0", "-ms", str(steps),
+                          "--no-plots", "--init-noise-device", "cpu"], cwd=ROOT,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = {}
+    for line in out.stdout.splitlines():
+        k, *vals = line.split()
+        got[k] = np.array([float(v) for v in vals])
+    exp = _check_rews_expected(golden("trace_cfg1"), steps, 0, 0)
+    for k, v in exp.items():
+        atol = ANGLE_ATOL if "angle" in k or "angels" in k else 0.0
+        np.testing.assert_allclose(got[k], v, rtol=2e-8 + RTOL, atol=atol + 1e-7, err_msg=k)

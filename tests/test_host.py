@@ -41,3 +41,16 @@ def test_output_set_is_free_only_when_unreferenced():
         assert not s.free()
         del x
         assert s.free()
+
+
+def test_cli_mirrors_reference_arguments():
+    """python -m marlnav_amd takes the reference's arguments with its
+    defaults (marlnav/__main__.py:49-132; utils.default_args restates them)."""
+    cli = importlib.import_module("marl-nav_amd.cli")
+    utils = importlib.import_module("marl-nav_amd.utils")
+    ns = vars(cli.build_parser().parse_args([]))
+    ref = vars(utils.default_args())
+    for k, v in ref.items():
+        assert ns[k] == v, k
+    assert cli.main([]) == 2          # training stays in the reference
+    assert cli.main(["-re"]) == 2     # and so does rendering

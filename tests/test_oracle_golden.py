@@ -172,3 +172,19 @@ def test_oracle_sincos_is_correctly_rounded():
     cr_c = np.array([np.float32(math.cos(float(v))) for v in th])
     assert (s == cr_s).mean() == 1.0 and (c == cr_c).mean() == 1.0
     assert np.signbit(orc.sincos(np.float32([-0.0]))[0][0])  # sin(-0) = -0
+
+
+def test_oracle_process_rewards_matches_reference():
+    """F5: oracle_discounted_returns against MAPPO._process_rewards run
+    unmodified (models.py:131-148), float64 within 1e-12."""
+    z = golden("process_rewards")
+    cases = meta("process_rewards")["cases"]
+    k = 0
+    while f"case{k}_rewards" in z:
+        m = cases[k]
+        ret, (mean, std) = orc.discounted_returns(z[f"case{k}_rewards"], z[f"case{k}_done"],
+                                                  m["gamma"])
+        np.testing.assert_allclose(ret, z[f"case{k}_returns"], rtol=1e-12, atol=1e-12)
+        assert abs(mean - float(z[f"case{k}_mean"])) <= 1e-12 * max(1.0, abs(mean))
+        k += 1
+    assert k == 3
