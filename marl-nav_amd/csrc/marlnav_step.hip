@@ -102,32 +102,128 @@ __device__ __forceinline__ float clamp_t(float x, float lo, float hi)
     return x > hi ? hi : x;
 }
 
+// Fast-path switches: 1 = guarded fast sequence (bit-exact where its guard
+// accepts, scripts/probes/fastmath_probe.hip; IEEE redo otherwise), 0 = the
+// IEEE operation. Measured on MI355X (scripts/graph_time.py, 65536x3x3,
+// 4096x16x32, 1024x3x8): the guards' compares and mask logic cost more than
+// the shorter sequences save, so the default build uses IEEE everywhere.
+#ifndef MARLNAV_FM_SQRT
+#define MARLNAV_FM_SQRT 0
+#endif
+#ifndef MARLNAV_FM_DIV2   // 2: exponent-range guard, 1: magnitude compares, 0: IEEE
+#define MARLNAV_FM_DIV2 0
+#endif
+#ifndef MARLNAV_FM_TERMS
+#define MARLNAV_FM_TERMS 0
+#endif
+
+// x == 0 or x = m * 2^e with e in [-59, 62] (|x| in [2^-60, 2^62)); NaN and
+// infinities pass (they also fail the denominators' guard)
+__device__ __forceinline__ bool exp_ok(float x)
+{
+    return (unsigned)(__builtin_amdgcn_frexp_expf(x) + 59) <= 121u;
+}
+
+// |x| in [lo, hi] or x == 0
+__device__ __forceinline__ bool mag_ok(float x, float lo, float hi)
+{
+    const float ax = fabsf(x);
+    return (ax >= lo && ax <= hi) || x == 0.0f;
+}
+
+// Correctly rounded sqrt for x in [2^-96, 2^96] or x == 0: hipcc's own
+// IEEE sequence (v_sqrt_f32, then the neighbour whose residual straddles x)
+// without its input scaling and special-value class fix-up, which only act
+// outside that range; `ok` is cleared outside it (the caller redoes the row
+// with the full sequence).
+__device__ __forceinline__ float sqrt_fast(float x, bool &ok)
+{
+    ok &= (x >= 0x1p-96f && x <= 0x1p96f) || x == 0.0f;
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float s_dn = __int_as_float(__float_as_int(s) - 1);
+    const float s_up = __int_as_float(__float_as_int(s) + 1);
+    const float r_dn = __builtin_fmaf(-s_dn, s, x);
+    const float r_up = __builtin_fmaf(-s_up, s, x);
+    s = r_dn <= 0.0f ? s_dn : s;
+    return r_up > 0.0f ? s_up : s;
+}
+
 // torch.cdist direct path (environment.py:271-274)
-__device__ __forceinline__ float pair_dist(float ox, float oy, float px, float py)
+template <bool FAST = false>
+__device__ __forceinline__ float pair_dist(float ox, float oy, float px, float py, bool &ok)
 {
     const float dx = px - ox, dy = py - oy;
 #if MARLNAV_ABLATE & 8
     return __builtin_amdgcn_sqrtf(__builtin_fmaf(dy, dy, dx * dx));
 #else
-    return __builtin_sqrtf(__builtin_fmaf(dy, dy, dx * dx));
+    if constexpr (FAST && MARLNAV_FM_SQRT)
+        return sqrt_fast(__builtin_fmaf(dy, dy, dx * dx), ok);
+    else
+        return __builtin_sqrtf(__builtin_fmaf(dy, dy, dx * dx));
 #endif
+}
+
+__device__ __forceinline__ float pair_dist(float ox, float oy, float px, float py)
+{
+    bool ok = true;
+    return pair_dist<false>(ox, oy, px, py, ok);
+}
+
+// Division by a wave-uniform constant c (a reward parameter): the same
+// core sequence as div2_fast with the reciprocal refined once per use site
+// (uniform, so once per wave). Guard: c in [2^-20, 2^20], the numerator zero
+// or in [2^-70, 2^70], so every intermediate stays normal; `ok` cleared
+// otherwise.
+struct DivC {
+    float c, r;
+};
+
+__device__ __forceinline__ DivC make_divc(float c, bool &ok)
+{
+    const float ac = fabsf(c);
+    ok &= ac >= 0x1p-20f && ac <= 0x1p20f;
+    float r = __builtin_amdgcn_rcpf(c);
+    r = __builtin_fmaf(__builtin_fmaf(-c, r, 1.0f), r, r);
+    return DivC{c, r};
+}
+
+__device__ __forceinline__ float div_c(float x, DivC d, bool &ok)
+{
+    ok &= mag_ok(x, 0x1p-70f, 0x1p70f);
+    float q = x * d.r;
+    q = __builtin_fmaf(__builtin_fmaf(-d.c, q, x), d.r, q);
+    return __builtin_fmaf(__builtin_fmaf(-d.c, q, x), d.r, q);
+}
+
+// 1 / den for den in [1, 2^96] (the bond term's 1 + sd^2): div2_fast's core.
+__device__ __forceinline__ float recip_fast(float den, bool &ok)
+{
+    ok &= den <= 0x1p96f;
+    float r = __builtin_amdgcn_rcpf(den);
+    r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    const float q = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    return __builtin_fmaf(__builtin_fmaf(-den, q, 1.0f), r, q);
 }
 
 // Two correctly rounded quotients over one denominator. This is hipcc's own
 // IEEE fp32 division sequence (reciprocal refined by one Newton step, two
 // residual corrections) with the v_div_scale / v_div_fixup range steps
-// dropped and the reciprocal shared. The caller guarantees den >= 1e-12 and
-// |x|, |y| <= ~den (den is the pair distance), so quotients lie in [-1, 1]
-// and, for den <= 2^96 and normal-or-zero numerators, no operand needs the
-// range steps; `ok` is cleared otherwise (huge or non-finite den, subnormal
-// numerators) and the caller redoes the row with IEEE division. Branch-free,
-// so consecutive pairs interleave. Verified bit-exact against IEEE division
-// on the GPU over this domain: scripts/probes/div_probe.hip.
+// dropped and the reciprocal shared. Those steps only matter when a quotient,
+// reciprocal or residual leaves the normal range; the guard keeps every
+// intermediate normal: den in [2^-60, 2^60] (den is a pair distance clamped
+// at 1e-12, so |x|, |y| <= den) and numerators zero or >= 2^-60 in magnitude.
+// `ok` is cleared otherwise and the caller redoes the row with IEEE division.
+// Branch-free, so consecutive pairs interleave. Checked bit-exact against
+// IEEE division on the GPU: scripts/probes/fastmath_probe.hip.
 __device__ __forceinline__ void div2_fast(float x, float y, float den, float *qx, float *qy,
                                           bool &ok)
 {
-    // 0x90: +-subnormal
-    ok &= (den <= 0x1p96f) & !__builtin_amdgcn_classf(x, 0x90) & !__builtin_amdgcn_classf(y, 0x90);
+#if MARLNAV_FM_DIV2 == 2
+    ok &= den >= 0x1p-60f && den <= 0x1p60f && exp_ok(x) && exp_ok(y);
+#else
+    ok &= den >= 0x1p-60f && den <= 0x1p60f && mag_ok(x, 0x1p-60f, 0x1p60f) &&
+          mag_ok(y, 0x1p-60f, 0x1p60f);
+#endif
     float r = __builtin_amdgcn_rcpf(den);
     r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
     float q = x * r;
@@ -151,7 +247,7 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
     const float nx = __fdividef(dx, den), ny = __fdividef(dy, den);
 #else
     float nx, ny;
-    if constexpr (FAST) {
+    if constexpr (FAST && MARLNAV_FM_DIV2 != 0) {
         div2_fast(dx, dy, den, &nx, &ny, ok);
     } else {
         nx = dx / den;
@@ -605,7 +701,7 @@ __device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
                                                   float *row, const MarlnavParams &pr, bool &ok)
 {
     const float cap = pr.cap_distance;
-    const float td = pair_dist(ox, oy, tge[0], tge[1]);
+    const float td = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
     const float ta = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, td, cap, ok);
     row[0] = ta;
     row[1] = td;
@@ -613,7 +709,7 @@ __device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
 #pragma unroll
     for (int j = 0; j < O; ++j) {
         const float px = obe[2 * j], py = obe[2 * j + 1];
-        const float d = pair_dist(ox, oy, px, py);
+        const float d = pair_dist<FAST>(ox, oy, px, py, ok);
         row[2 + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
         row[2 + O + j] = d;
         if (TERMS) {
@@ -627,7 +723,7 @@ __device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
     for (int j = 0; j < A - 1; ++j) {
         const int m = j + (j >= a ? 1 : 0);
         const float px = sts[5 * m], py = sts[5 * m + 1];
-        const float d = pair_dist(ox, oy, px, py);
+        const float d = pair_dist<FAST>(ox, oy, px, py, ok);
         row[2 + 2 * O + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
         row[2 + 2 * O + (A - 1) + j] = d;
         if (TERMS) {
@@ -639,14 +735,30 @@ __device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
     RowOut out{0.0f, 0.0f, 0u};
     if (TERMS) {
         const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
-        const float dsc = (band < pr.max_at_prop_d ? band : pr.max_at_prop_d) / pr.max_at_prop_d;
-        const float soft = -1.0f * (td / pr.init_dist);
         const float ideal = pr.ideal_dist, sharp = pr.bond_sharpness;
-        const float bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [ideal, sharp](float d) {
-            const float sd = (d - ideal) / sharp;
-            return 1.0f / (1.0f + sd * sd);
-        });
-        const float bondm = bond / (float)(A - 1);
+        const float bandc = band < pr.max_at_prop_d ? band : pr.max_at_prop_d;
+        float dsc, soft, bondm;
+        if constexpr (FAST && MARLNAV_FM_TERMS) {
+            const DivC d_mapd = make_divc(pr.max_at_prop_d, ok);
+            const DivC d_init = make_divc(pr.init_dist, ok);
+            const DivC d_sharp = make_divc(sharp, ok);
+            const DivC d_am1 = make_divc((float)(A - 1), ok);
+            dsc = div_c(bandc, d_mapd, ok);
+            soft = -1.0f * div_c(td, d_init, ok);
+            const float bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [&](float d) {
+                const float sd = div_c(d - ideal, d_sharp, ok);
+                return recip_fast(1.0f + sd * sd, ok);
+            });
+            bondm = div_c(bond, d_am1, ok);
+        } else {
+            dsc = bandc / pr.max_at_prop_d;
+            soft = -1.0f * (td / pr.init_dist);
+            const float bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [ideal, sharp](float d) {
+                const float sd = (d - ideal) / sharp;
+                return 1.0f / (1.0f + sd * sd);
+            });
+            bondm = bond / (float)(A - 1);
+        }
         const float risk = (ob_risk || ag_risk) ? 1.0f : 0.0f;
         float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
         float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
@@ -1305,7 +1417,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
 #pragma unroll
                 for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
                 const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
-                b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
+                bool okq = MARLNAV_FM_TERMS != 0;                                    // torch.mean (:233)
+                float rmean = MARLNAV_FM_TERMS ? div_c(rsum, make_divc((float)A, okq), okq) : 0.0f;
+                if (__builtin_expect(!okq, 0)) rmean = rsum / (float)A;
+                b.reward[e] = rmean;
 
                 float step_num = cur[TP::SN + lane] + 1.0f;        // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
@@ -1531,7 +1646,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     const float cap = pr.cap_distance;
     SplitTerms t{0u, 0, 0.0f, 0.0f};
     {
-        const float d = pair_dist(ox, oy, tge[0], tge[1]);
+        const float d = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
         const float ang = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, d, cap, ok);
         t.ta = ang;
         t.td = d;
@@ -1545,7 +1660,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
         const int j = q + LPR * i;
         if (O % LPR == 0 || j < O) {
             const float px = obe[2 * j], py = obe[2 * j + 1];
-            const float d = pair_dist(ox, oy, px, py);
+            const float d = pair_dist<FAST>(ox, oy, px, py, ok);
             orow[2 + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
             orow[2 + O + j] = d;
             if (TERMS)
@@ -1558,14 +1673,19 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
         if ((A - 1) % LPR == 0 || kx < A - 1) {
             const int m = kx + (kx >= a ? 1 : 0);
             const float px = sts[5 * m], py = sts[5 * m + 1];
-            const float d = pair_dist(ox, oy, px, py);
+            const float d = pair_dist<FAST>(ox, oy, px, py, ok);
             orow[2 + 2 * O + kx] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
             orow[2 + 2 * O + (A - 1) + kx] = d;
             if (TERMS) {
                 t.fl |= (d < pr.ag_risk_dist ? 4u : 0u) | (d < pr.ag_coll_dist ? 8u : 0u);
                 t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
-                const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
-                bond_row[kx] = 1.0f / (1.0f + sd * sd);
+                if constexpr (FAST && MARLNAV_FM_TERMS) {
+                    const float sd = div_c(d - pr.ideal_dist, make_divc(pr.bond_sharpness, ok), ok);
+                    bond_row[kx] = recip_fast(1.0f + sd * sd, ok);
+                } else {
+                    const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
+                    bond_row[kx] = 1.0f / (1.0f + sd * sd);
+                }
             }
         }
     }
@@ -1687,13 +1807,23 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
             if (row_on && q == 0) {
                 const float head = fabsf(t.ta) < pr.max_angle_diff ? 1.0f : 0.0f;
                 const float bandf = (float)band;
-                const float dsc = (bandf < pr.max_at_prop_d ? bandf : pr.max_at_prop_d) / pr.max_at_prop_d;
-                const float soft = -1.0f * (t.td / pr.init_dist);
+                const float bandc = bandf < pr.max_at_prop_d ? bandf : pr.max_at_prop_d;
                 float bv[A - 1];
 #pragma unroll
                 for (int i = 0; i < A - 1; ++i) bv[i] = brow[i];
                 const float bond = torch_row_sum_r<A - 1>(bv, [](float x) { return x; });
-                const float bondm = bond / (float)(A - 1);
+                bool okl = MARLNAV_FM_TERMS != 0;
+                float dsc = 0.0f, soft = 0.0f, bondm = 0.0f;
+                if (MARLNAV_FM_TERMS) {
+                    dsc = div_c(bandc, make_divc(pr.max_at_prop_d, okl), okl);
+                    soft = -1.0f * div_c(t.td, make_divc(pr.init_dist, okl), okl);
+                    bondm = div_c(bond, make_divc((float)(A - 1), okl), okl);
+                }
+                if (__builtin_expect(!okl, 0)) {
+                    dsc = bandc / pr.max_at_prop_d;
+                    soft = -1.0f * (t.td / pr.init_dist);
+                    bondm = bond / (float)(A - 1);
+                }
                 const float risk = (fl & 5u) ? 1.0f : 0.0f;
                 float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
                 float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
@@ -1735,7 +1865,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
 #pragma unroll
             for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
             const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
-            b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
+            bool okq = MARLNAV_FM_TERMS != 0;                                    // torch.mean (:233)
+            float rmean = MARLNAV_FM_TERMS ? div_c(rsum, make_divc((float)A, okq), okq) : 0.0f;
+            if (__builtin_expect(!okq, 0)) rmean = rsum / (float)A;
+            b.reward[e] = rmean;
             float step_num = sn_in + 1.0f;                     // :96
             const bool truncated = step_num > pr.trunc_after;  // :97
             const bool term_old = term_in != 0u;
