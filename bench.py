@@ -155,12 +155,20 @@ def main():
     if world != a.gpus:
         if world > 1:
             raise SystemExit(f"WORLD_SIZE={world} but --gpus {a.gpus}")
+    # MARLNAV_BENCH_BACKEND=gloo rehearses the N>1 path on fewer GPUs than
+    # ranks (ranks share devices; reductions on the host)
+    backend = os.environ.get("MARLNAV_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
+    red_dev = device if backend == "nccl" else None
 
     import marlnav_amd as pkg
     P, A, O = a.envs, a.agents, a.obstacles
@@ -182,7 +190,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    dt = pkg.shard.max_over_ranks(dt, device)
+    dt = pkg.shard.max_over_ranks(dt, red_dev)
 
     kern_avg, kern_med = kernel_time_us(env, actions)
     per_env = alg_bytes_per_env(A, O)
@@ -202,7 +210,7 @@ def main():
                           f"in {secs:.1f} s after 1 warm-up step; host os.cpu_count()="
                           f"{os.cpu_count()}")}
 
-    counters = pkg.shard.sum_over_ranks([env._num_trunc, env._num_col, env._num_tar], device)
+    counters = pkg.shard.sum_over_ranks([env._num_trunc, env._num_col, env._num_tar], red_dev)
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node) at 3 agents; 1/2/4/8-GPU scaling + %HBM roofline",

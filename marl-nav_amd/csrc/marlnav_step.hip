@@ -2188,6 +2188,9 @@ const SplitVariant kSplitVariants[] = {
     MARLNAV_SPLIT_VARIANT(16, 32, 4, true),
     MARLNAV_SPLIT_VARIANT(3, 8, 4, false),
     MARLNAV_SPLIT_VARIANT(3, 3, 4, false),
+#ifdef MARLNAV_SPLIT33_LPR2
+    MARLNAV_SPLIT_VARIANT(3, 3, 2, false),
+#endif
 };
 #undef MARLNAV_SPLIT_VARIANT
 
