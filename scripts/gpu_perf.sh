@@ -26,8 +26,8 @@ import csv, glob, collections
 rows = list(csv.DictReader(open(glob.glob("gpurun_out/prof_*/run_kernel_trace.csv")[-1])))
 by = collections.defaultdict(list)
 for r in rows:
-    if "wave_kernel" in r["Kernel_Name"]:
-        by[(r["Kernel_Name"][:60], r["Grid_Size"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    if any(k in r["Kernel_Name"] for k in ("wave_kernel", "tile_kernel", "split_kernel")):
+        by[(r["Kernel_Name"][:60], r.get("Grid_Size", r.get("Grid_Size_X")))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k, v in by.items():
     v.sort()
     print("rocprof", k[1], "grid", "n=%d median_us=%.2f min=%.2f" % (len(v), v[len(v)//2], v[0]), k[0])
