@@ -102,17 +102,20 @@ __device__ __forceinline__ float clamp_t(float x, float lo, float hi)
     return x > hi ? hi : x;
 }
 
-// Fast-path switches: 1 = guarded fast sequence (bit-exact where its guard
-// accepts, scripts/probes/fastmath_probe.hip; IEEE redo otherwise), 0 = the
-// IEEE operation. Measured on MI355X (scripts/graph_time.py, 65536x3x3,
-// 4096x16x32, 1024x3x8): the guards' compares and mask logic cost more than
-// the shorter sequences save, so the default build uses IEEE everywhere.
+// Fast-path switches for the pair math in FAST mode: 1 = the shortened
+// sequence (bit-exact inside its guard, scripts/probes/fastmath_probe.hip),
+// 0 = the IEEE operation. The tile kernels enter FAST mode only for a wave
+// whose every coordinate passed coords_in_range() (which implies every
+// per-pair guard), so there the guards are dead code. Kernels that evaluate
+// the guards per pair (wave/split kernels) were measured slower with them and
+// run IEEE-only (kGuardedFast).
 #ifndef MARLNAV_FM_SQRT
-#define MARLNAV_FM_SQRT 0
+#define MARLNAV_FM_SQRT 1
 #endif
 #ifndef MARLNAV_FM_DIV2   // 2: exponent-range guard, 1: magnitude compares, 0: IEEE
-#define MARLNAV_FM_DIV2 0
+#define MARLNAV_FM_DIV2 1
 #endif
+constexpr bool kGuardedFast = false;
 #ifndef MARLNAV_FM_TERMS
 #define MARLNAV_FM_TERMS 0
 #endif
@@ -129,6 +132,33 @@ __device__ __forceinline__ bool mag_ok(float x, float lo, float hi)
 {
     const float ax = fabsf(x);
     return (ax >= lo && ax <= hi) || x == 0.0f;
+}
+
+// A coordinate the fast pair math accepts without per-pair guards: zero or
+// |c| in [2^-20, 2^40]. If every position a row uses satisfies it, every
+// nonzero difference is >= 2^-43 and <= 2^41, so each pair's squared
+// distance lies in [2^-86, 2^83] (sqrt_fast guard [2^-96, 2^96]), each
+// distance in [1e-12 clamp, 2^42] and each numerator zero or in
+// [2^-43, 2^41] (div2_fast guard [2^-60, 2^60]).
+__device__ __forceinline__ bool coord_ok(float c) { return mag_ok(c, 0x1p-20f, 0x1p40f); }
+
+// coord_ok over a full tile's staged obstacle (NOB floats) and target (NTG)
+// coordinates, spread over the wave's lanes
+template <int NOB, int NTG>
+__device__ __forceinline__ bool tile_coords_ok(const float *ob, const float *tg, unsigned lane)
+{
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k * 64 < NOB; ++k) {
+        const int i = k * 64 + (int)lane;
+        if ((k + 1) * 64 <= NOB || i < NOB) ok = ok && coord_ok(ob[i]);
+    }
+#pragma unroll
+    for (int k = 0; k * 64 < NTG; ++k) {
+        const int i = k * 64 + (int)lane;
+        if ((k + 1) * 64 <= NTG || i < NTG) ok = ok && coord_ok(tg[i]);
+    }
+    return ok;
 }
 
 // Correctly rounded sqrt for x in [2^-96, 2^96] or x == 0: hipcc's own
@@ -964,7 +994,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
             RowOut ro;
             if constexpr (REGROW) {
                 bool ok = true;
-                ro = observe_row_regs<A_T, O_T, !OBS_ONLY, true>(
+                ro = observe_row_regs<A_T, O_T, !OBS_ONLY, kGuardedFast>(
                     st + 5 * A * el, ob + 2 * S * el, tg + 2 * el, a, rowv, pr, ok);
                 if (__builtin_expect(__ballot(!ok) != 0ull, 0) && !ok)  // IEEE redo, rare
                     ro = observe_row_regs<A_T, O_T, !OBS_ONLY, false>(
@@ -1042,7 +1072,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                 if (row_on && envbits[el]) {
                     if constexpr (REGROW) {
                         bool ok = true;
-                        observe_row_regs<A_T, O_T, false, true>(st + 5 * A * el, ob + 2 * S * el,
+                        observe_row_regs<A_T, O_T, false, kGuardedFast>(st + 5 * A * el, ob + 2 * S * el,
                                                                 tg + 2 * el, a, rowv, pr, ok);
                         if (!ok)
                             observe_row_regs<A_T, O_T, false, false>(
@@ -1364,28 +1394,34 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
 
         // ---- observations of the moved state + reward terms (:99-100)
         float rowv[RPL][D];
+        // wave-uniform choice of the pair math: the short sqrt / shared-
+        // reciprocal division sequences when every coordinate of the tile
+        // passes coord_ok (then they equal the IEEE results), IEEE otherwise
+        bool cok = true;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) cok = cok && (!row_on[q] || (coord_ok(ox[q]) && coord_ok(oy[q])));
+        cok = cok && tile_coords_ok<W * O * 2, W * 2>(cur + TP::OB, cur + TP::TG, lane);
+        const bool fast = ne == W && __ballot(!cok) == 0ull;
         if (!(MARLNAV_ABLATE & 16) && (int)lane < L) {
-            bool ok[RPL];
             RowOut ro[RPL];
+            if (__builtin_expect(fast, 1)) {
 #pragma unroll
-            for (int q = 0; q < RPL; ++q) {
-                ok[q] = true;
-                ro[q] = observe_row_own<A, O, !OBS_ONLY, true>(
-                    st + 5 * A * rel[q], cur + TP::OB + 2 * O * rel[q], cur + TP::TG + 2 * rel[q],
-                    a, ox[q], oy[q], dx[q], dy[q], rowv[q], pr, ok[q]);
-                ok[q] = ok[q] || !row_on[q];  // rows past the tile: garbage, unused
-            }
-            bool all_ok = true;
+                for (int q = 0; q < RPL; ++q) {
+                    bool unused = true;  // guards implied by coords_in_range
+                    ro[q] = observe_row_own<A, O, !OBS_ONLY, true>(
+                        st + 5 * A * rel[q], cur + TP::OB + 2 * O * rel[q],
+                        cur + TP::TG + 2 * rel[q], a, ox[q], oy[q], dx[q], dy[q], rowv[q], pr,
+                        unused);
+                }
+            } else {
 #pragma unroll
-            for (int q = 0; q < RPL; ++q) all_ok = all_ok && ok[q];
-            if (__builtin_expect(__ballot(!all_ok) != 0ull, 0)) {  // IEEE redo, rare
-#pragma unroll
-                for (int q = 0; q < RPL; ++q)
-                    if (!ok[q])
-                        ro[q] = observe_row_own<A, O, !OBS_ONLY, false>(
-                            st + 5 * A * rel[q], cur + TP::OB + 2 * O * rel[q],
-                            cur + TP::TG + 2 * rel[q], a, ox[q], oy[q], dx[q], dy[q], rowv[q], pr,
-                            ok[q]);
+                for (int q = 0; q < RPL; ++q) {
+                    bool unused = true;
+                    ro[q] = observe_row_own<A, O, !OBS_ONLY, false>(
+                        st + 5 * A * rel[q], cur + TP::OB + 2 * O * rel[q],
+                        cur + TP::TG + 2 * rel[q], a, ox[q], oy[q], dx[q], dy[q], rowv[q], pr,
+                        unused);
+                }
             }
             if (!OBS_ONLY) {
 #pragma unroll
@@ -1479,20 +1515,28 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
             // ---- observations of re-initialised envs (:105)
             if (finmask) {
                 wave_sync();
+                bool cok2 = true;
+#pragma unroll
+                for (int q = 0; q < RPL; ++q)
+                    cok2 = cok2 && (!row_on[q] || (coord_ok(st[5 * rix[q]]) &&
+                                                   coord_ok(st[5 * rix[q] + 1])));
+                cok2 = cok2 && tile_coords_ok<W * O * 2, W * 2>(cur + TP::OB, cur + TP::TG, lane);
+                const bool fast2 = ne == W && __ballot(!cok2) == 0ull;
 #pragma unroll
                 for (int q = 0; q < RPL; ++q) {
                     if (row_on[q] && ((finmask >> rel[q]) & 1u)) {
-                        bool ok = true;
+                        bool unused = true;
                         const float *s = st + 5 * rix[q];
                         const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
                         const float *sts = st + 5 * A * rel[q];
                         const float *obe = cur + TP::OB + 2 * O * rel[q];
                         const float *tge = cur + TP::TG + 2 * rel[q];
-                        observe_row_own<A, O, false, true>(sts, obe, tge, a, rx, ry, rdx, rdy,
-                                                           rowv[q], pr, ok);
-                        if (!ok)
+                        if (fast2)
+                            observe_row_own<A, O, false, true>(sts, obe, tge, a, rx, ry, rdx, rdy,
+                                                               rowv[q], pr, unused);
+                        else
                             observe_row_own<A, O, false, false>(sts, obe, tge, a, rx, ry, rdx,
-                                                                rdy, rowv[q], pr, ok);
+                                                                rdy, rowv[q], pr, unused);
                     }
                 }
             }
@@ -1792,7 +1836,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
     float *brow = wl + SP::BOND + rowc * (A - 1);
     {
         bool ok = true;
-        SplitTerms t = split_pairs<A, O, LPR, !OBS_ONLY, true>(sts, obe, tge, a, q, ox, oy, dx, dy,
+        SplitTerms t = split_pairs<A, O, LPR, !OBS_ONLY, kGuardedFast>(sts, obe, tge, a, q, ox, oy, dx, dy,
                                                              orow, brow, pr, ok);
         ok = ok || !row_on;
         if (__builtin_expect(__ballot(!ok) != 0ull, 0)) {  // IEEE redo, rare
@@ -1931,7 +1975,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
             const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
             bool ok = true;
             if (redo)
-                split_pairs<A, O, LPR, false, true>(sts, obe, tge, a, q, rx, ry, rdx, rdy, orow,
+                split_pairs<A, O, LPR, false, kGuardedFast>(sts, obe, tge, a, q, rx, ry, rdx, rdy, orow,
                                                    brow, pr, ok);
             ok = ok || !redo;
             if (__ballot(!ok) != 0ull && redo)

@@ -439,3 +439,41 @@ def test_cli_reward_check_matches_reference(pkg):
     for k, v in exp.items():
         atol = ANGLE_ATOL if "angle" in k or "angels" in k else 0.0
         np.testing.assert_allclose(got[k], v, rtol=2e-8 + RTOL, atol=atol + 1e-7, err_msg=k)
+
+
+@pytest.mark.parametrize("P,O", [(16384, 3), (20480, 8)])
+def test_extreme_coordinates_take_the_exact_path(pkg, P, O):
+    """Tiles holding coordinates outside the fast pair math's range (tiny,
+    huge, coincident points) fall back to IEEE sqrt/division for the whole
+    wave; every env still equals the oracle bit for bit."""
+    g = torch.Generator().manual_seed(O)
+    env = make_env(pkg, P, 3, O, episode_len=9, seed=5)
+    st = env.states.cpu().clone()
+    ob = env.obstacles.cpu().clone()
+    tg = env.target.cpu().clone()
+    st[5, 1, :2] = torch.tensor([1e-25, 3e-30])          # tiny positions
+    st[6, 0, :2] = torch.tensor([2e-39, 0.0])            # subnormal
+    st[7, 2, :2] = st[7, 0, :2]                          # coincident agents
+    ob[40, 0] = torch.tensor([1e30, 5.0])                # huge obstacle
+    tg[100, 0] = torch.tensor([0.0, 1e-22])
+    st[300, 1, :2] = torch.tensor([3e12, -7e11])          # beyond 2^40
+    env.states, env.obstacles, env.target = st, ob, tg
+    dm, pr = oracle_params(env)
+    form = np_(env._formation)
+    s, o, t = st.numpy(), ob.numpy(), tg.numpy()
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    for k in range(3):
+        acts = (torch.rand(P, 3, 2, generator=g) - 0.5)
+        exp = orc.step(dm, pr, s, o, t, sn, te, acts.numpy(), formation=form, step_idx=k + 1)
+        obs, rew, term, trunc = env.step(acts.to(DEV))
+        where = f"P{P} O{O} step {k + 1}"
+        np.testing.assert_array_equal(np_(env.states), exp["states"], where)
+        np.testing.assert_array_equal(np_(rew), exp["reward"], where)
+        np.testing.assert_array_equal(np_(term), exp["terminated"], where)
+        got = np_(obs._packed)
+        np.testing.assert_array_equal(got[..., 1], exp["obs"][..., 1], where)  # distances exact
+        fg, fo = orc.split_obs(got, 3, O), orc.split_obs(exp["obs"], 3, O)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, where=where)
+        s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
+                                            "terminates"))
