@@ -1629,6 +1629,11 @@ struct SplitPlan {
 
 __host__ __device__ constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
 
+// the fast pair math pays for its per-wave coordinate check only with many
+// pairs per lane (measured: A16/O32 yes, A3/O3 and A3/O8 at LPR 4 no)
+template <int A, int O, int LPR>
+constexpr bool kSplitFastMath = SplitPlan<A, O, LPR>::NOB + SplitPlan<A, O, LPR>::NAG >= 6;
+
 // global -> LDS copy of NB bytes whose source is ALIGN-byte aligned: 16-byte
 // LDS-DMA when possible, else dword LDS-DMA (NB % 4 == 0, ALIGN % 4 == 0).
 template <int NB, int ALIGN>
@@ -1835,15 +1840,22 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
     float *orow = wl + SP::OBS + rowc * D;
     float *brow = wl + SP::BOND + rowc * (A - 1);
     {
-        bool ok = true;
-        SplitTerms t = split_pairs<A, O, LPR, !OBS_ONLY, kGuardedFast>(sts, obe, tge, a, q, ox, oy, dx, dy,
-                                                             orow, brow, pr, ok);
-        ok = ok || !row_on;
-        if (__builtin_expect(__ballot(!ok) != 0ull, 0)) {  // IEEE redo, rare
-            ok = true;
-            t = split_pairs<A, O, LPR, !OBS_ONLY, false>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
-                                                        brow, pr, ok);
+        // wave-uniform choice of the pair math (coord_ok, as in tile_kernel);
+        // worth its check only when each lane evaluates many pairs
+        bool fast = false;
+        if constexpr (kSplitFastMath<A, O, LPR>) {
+            const bool cok = (!row_on || (coord_ok(ox) && coord_ok(oy))) &&
+                             tile_coords_ok<EPW * O * 2, EPW * 2>(wl + SP::OB, wl + SP::TG, lane);
+            fast = ne == EPW && __ballot(!cok) == 0ull;
         }
+        bool unused = true;
+        SplitTerms t;
+        if (__builtin_expect(fast, 1))
+            t = split_pairs<A, O, LPR, !OBS_ONLY, true>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
+                                                       brow, pr, unused);
+        else
+            t = split_pairs<A, O, LPR, !OBS_ONLY, false>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
+                                                        brow, pr, unused);
         if (!OBS_ONLY) {
             const unsigned fl = lpr_or<LPR>(t.fl);
             const int band = lpr_sum<LPR>(t.band);
@@ -1973,14 +1985,21 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
             const bool redo = row_on && ((finmask >> el) & 1u);
             const float *s = st + 5 * rowc;
             const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
-            bool ok = true;
-            if (redo)
-                split_pairs<A, O, LPR, false, kGuardedFast>(sts, obe, tge, a, q, rx, ry, rdx, rdy, orow,
-                                                   brow, pr, ok);
-            ok = ok || !redo;
-            if (__ballot(!ok) != 0ull && redo)
-                split_pairs<A, O, LPR, false, false>(sts, obe, tge, a, q, rx, ry, rdx, rdy, orow,
-                                                    brow, pr, ok);
+            bool fast2 = false;
+            if constexpr (kSplitFastMath<A, O, LPR>) {
+                const bool cok2 = (!redo || (coord_ok(rx) && coord_ok(ry))) &&
+                                  tile_coords_ok<EPW * O * 2, EPW * 2>(wl + SP::OB, wl + SP::TG, lane);
+                fast2 = ne == EPW && __ballot(!cok2) == 0ull;
+            }
+            bool unused = true;
+            if (redo) {
+                if (fast2)
+                    split_pairs<A, O, LPR, false, true>(sts, obe, tge, a, q, rx, ry, rdx, rdy,
+                                                       orow, brow, pr, unused);
+                else
+                    split_pairs<A, O, LPR, false, false>(sts, obe, tge, a, q, rx, ry, rdx, rdy,
+                                                        orow, brow, pr, unused);
+            }
         }
     }
     STAMP(5);

@@ -441,13 +441,14 @@ def test_cli_reward_check_matches_reference(pkg):
         np.testing.assert_allclose(got[k], v, rtol=2e-8 + RTOL, atol=atol + 1e-7, err_msg=k)
 
 
-@pytest.mark.parametrize("P,O", [(16384, 3), (20480, 8)])
-def test_extreme_coordinates_take_the_exact_path(pkg, P, O):
+@pytest.mark.parametrize("P,A,O", [(16384, 3, 3), (20480, 3, 8), (4096, 3, 3), (1024, 3, 8),
+                                   (512, 16, 32)])
+def test_extreme_coordinates_take_the_exact_path(pkg, P, A, O):
     """Tiles holding coordinates outside the fast pair math's range (tiny,
     huge, coincident points) fall back to IEEE sqrt/division for the whole
     wave; every env still equals the oracle bit for bit."""
-    g = torch.Generator().manual_seed(O)
-    env = make_env(pkg, P, 3, O, episode_len=9, seed=5)
+    g = torch.Generator().manual_seed(O + A)
+    env = make_env(pkg, P, A, O, episode_len=9, seed=5)
     st = env.states.cpu().clone()
     ob = env.obstacles.cpu().clone()
     tg = env.target.cpu().clone()
@@ -464,16 +465,16 @@ def test_extreme_coordinates_take_the_exact_path(pkg, P, O):
     sn = np.zeros(P, np.float32)
     te = np.zeros(P, np.bool_)
     for k in range(3):
-        acts = (torch.rand(P, 3, 2, generator=g) - 0.5)
+        acts = (torch.rand(P, A, 2, generator=g) - 0.5)
         exp = orc.step(dm, pr, s, o, t, sn, te, acts.numpy(), formation=form, step_idx=k + 1)
         obs, rew, term, trunc = env.step(acts.to(DEV))
-        where = f"P{P} O{O} step {k + 1}"
+        where = f"P{P} A{A} O{O} step {k + 1}"
         np.testing.assert_array_equal(np_(env.states), exp["states"], where)
         np.testing.assert_array_equal(np_(rew), exp["reward"], where)
         np.testing.assert_array_equal(np_(term), exp["terminated"], where)
         got = np_(obs._packed)
         np.testing.assert_array_equal(got[..., 1], exp["obs"][..., 1], where)  # distances exact
-        fg, fo = orc.split_obs(got, 3, O), orc.split_obs(exp["obs"], 3, O)
+        fg, fo = orc.split_obs(got, A, O), orc.split_obs(exp["obs"], A, O)
         assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, where=where)
         s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))
