@@ -1168,7 +1168,7 @@ __device__ __forceinline__ T in_sgpr(T p)
 struct StepPtrs {
     float *states, *obstacles, *target, *step_num, *obs, *reward;
     uint8_t *terminates, *terminated, *truncated;
-    const float *actions;
+    const float *actions, *formation;
 };
 
 __device__ __forceinline__ StepPtrs load_ptrs(KArgsK *K)
@@ -1184,6 +1184,7 @@ __device__ __forceinline__ StepPtrs load_ptrs(KArgsK *K)
     q.terminated = K->a.b.terminated;
     q.truncated = K->a.b.truncated;
     q.actions = K->a.b.actions;
+    q.formation = K->a.b.formation;
     return q;
 }
 
@@ -1260,9 +1261,63 @@ struct TilePlan {
     static constexpr int TM = (SN + W + 3) & ~3;                  // (W,) bytes
     static constexpr int STAGE = (TM + (W + 3) / 4 + 3) & ~3;
     static constexpr int RED = STAGE;                             // (R, 4)
-    static constexpr int FLOATS = RED + 4 * R;
+    static constexpr int FORM = RED + 4 * R;                      // 5A + 2 (native re-init)
+    static constexpr int LIST = (FORM + 5 * A + 2 + 3) & ~3;      // (W,) finished envs
+    static constexpr int FLOATS = (LIST + W + 3) & ~3;
+    // re-observed rows reuse RED once the env phase has read it: this many
+    // finished envs' (A, D) rows per chunk
+    static constexpr int REOBS_ENVS = (4 * R) / (A * D) > 0 ? (4 * R) / (A * D) : 1;
+    static_assert((4 * R) / (A * D) > 0, "RED must hold one env's re-observed rows");
     static_assert(W <= 64, "one lane per env in the per-env phase");
 };
+
+// Re-observation of the finished envs' rows (environment.py:105) spread over
+// the wave: one (row, pair) item per lane per pass instead of one whole row
+// per lane, so a tile with a few finished envs pays about one pair's latency
+// instead of a row's. st/ob/tg: the tile's re-initialised LDS state; list:
+// the tile indices of the nfin finished envs (this chunk); results go to
+// obsr[(rank * A + agent) * D + slot] in the packed Observations order.
+template <int A, int O, bool FAST>
+__device__ __forceinline__ void reobs_spread(const float *st, const float *ob, const float *tg,
+                                             const int *list, int nfin, float *obsr, float cap,
+                                             unsigned lane)
+{
+    constexpr int NP = 1 + O + (A - 1), D = 2 + 2 * O + 2 * (A - 1);
+    const int nw = nfin * A * NP;
+    for (int base = 0; base < nw; base += 64) {
+        const int w = base + (int)lane;
+        if (w < nw) {
+            const int fe = w / (A * NP), rem = w - fe * (A * NP);
+            const int ag = rem / NP, p = rem - ag * NP;
+            const int env = list[fe];
+            const int row = env * A + ag;
+            const float *s = st + 5 * row;
+            const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
+            const float *pt;
+            int sa, sd;
+            if (p == 0) {                 // target
+                pt = tg + 2 * env;
+                sa = 0;
+                sd = 1;
+            } else if (p <= O) {          // obstacle p - 1
+                pt = ob + 2 * (env * O + p - 1);
+                sa = 1 + p;
+                sd = 1 + O + p;
+            } else {                      // other agent k, skipping self
+                const int kx = p - O - 1;
+                pt = st + 5 * (env * A + kx + (kx >= ag ? 1 : 0));
+                sa = 2 + 2 * O + kx;
+                sd = 2 + 2 * O + (A - 1) + kx;
+            }
+            bool unused = true;
+            const float px = pt[0], py = pt[1];
+            const float d = pair_dist<FAST>(ox, oy, px, py, unused);
+            float *o = obsr + (fe * A + ag) * D;
+            o[sa] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, unused);
+            o[sd] = d;
+        }
+    }
+}
 
 // Stage tile `tile` into `buf`: LDS-DMA for a full tile (returns without
 // waiting), plain copies for a partial last tile.
@@ -1282,6 +1337,9 @@ __device__ __forceinline__ void tile_stage(const StepPtrs &b, int64_t P, int64_t
             glds_span<W * 4>(b.step_num + e0, buf + TP::SN, lane);
             glds_span<W>(b.terminates + e0, buf + TP::TM, lane);
         }
+        // native re-init template (utils.py:375-398): a finished env copies it
+        // from LDS instead of waiting on a global load
+        if (!OBS_ONLY && b.formation) glds_span<(5 * A + 2) * 4>(b.formation, buf + TP::FORM, lane);
     } else {
         const int ne = (int)(P - e0), nr = ne * A;
         copy_span(b.states + e0 * (A * 5), buf + TP::ST, nr * 5, (int)lane);
@@ -1291,6 +1349,7 @@ __device__ __forceinline__ void tile_stage(const StepPtrs &b, int64_t P, int64_t
         if (!OBS_ONLY) {
             copy_span(b.step_num + e0, buf + TP::SN, ne, (int)lane);
             copy_span(b.terminates + e0, reinterpret_cast<uint8_t *>(buf + TP::TM), ne, (int)lane);
+            if (b.formation) copy_span(b.formation, buf + TP::FORM, 5 * A + 2, (int)lane);
         }
     }
 }
@@ -1330,6 +1389,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
     const MarlnavParams pr = load_params(K);
     const int el = (int)lane / A, a = (int)lane - el * A;
     unsigned c_trunc = 0, c_col = 0, c_tar = 0;
+    unsigned n_fin = 0;  // finished envs of this tile (stamps builds record it)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
     wave_sync();
     STAMP(1);
@@ -1492,7 +1552,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
                         tgl[0] = ft[2 * e];
                         tgl[1] = ft[2 * e + 1];
                     } else {
-                        native_fresh_env<NOISY>(A, O, p, kl->a.b.formation,
+                        native_fresh_env<NOISY>(A, O, p, cur + TP::FORM,
                                                 (uint64_t)(kl->a.env_offset + e), kl->a.step_idx,
                                                 s5, obl, tgl);
                     }
@@ -1507,6 +1567,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
                 ta_l = all_in;
             }
             const uint64_t finmask = __ballot(fin);
+            n_fin = __popcll(finmask);
             c_trunc += __popcll(__ballot(tr_l));
             c_col += __popcll(__ballot(co_l));
             c_tar += __popcll(__ballot(ta_l));
@@ -1514,6 +1575,11 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
 
             // ---- observations of re-initialised envs (:105)
             if (finmask) {
+                int *list = reinterpret_cast<int *>(cur + TP::LIST);
+                if (fin)
+                    list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] =
+                        (int)lane;
                 wave_sync();
                 bool cok2 = true;
 #pragma unroll
@@ -1522,22 +1588,30 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
                                                    coord_ok(st[5 * rix[q] + 1])));
                 cok2 = cok2 && tile_coords_ok<W * O * 2, W * 2>(cur + TP::OB, cur + TP::TG, lane);
                 const bool fast2 = ne == W && __ballot(!cok2) == 0ull;
+                const int nfin = (int)__popcll(finmask);
+                float *obsr = cur + TP::RED;  // free once the env phase has read it
+                int rank[RPL];
 #pragma unroll
-                for (int q = 0; q < RPL; ++q) {
-                    if (row_on[q] && ((finmask >> rel[q]) & 1u)) {
-                        bool unused = true;
-                        const float *s = st + 5 * rix[q];
-                        const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
-                        const float *sts = st + 5 * A * rel[q];
-                        const float *obe = cur + TP::OB + 2 * O * rel[q];
-                        const float *tge = cur + TP::TG + 2 * rel[q];
-                        if (fast2)
-                            observe_row_own<A, O, false, true>(sts, obe, tge, a, rx, ry, rdx, rdy,
-                                                               rowv[q], pr, unused);
-                        else
-                            observe_row_own<A, O, false, false>(sts, obe, tge, a, rx, ry, rdx,
-                                                                rdy, rowv[q], pr, unused);
-                    }
+                for (int q = 0; q < RPL; ++q)
+                    rank[q] = (int)__popcll(finmask & ((1ull << rel[q]) - 1ull));
+                for (int c0 = 0; c0 < nfin; c0 += TP::REOBS_ENVS) {
+                    const int nc = nfin - c0 < TP::REOBS_ENVS ? nfin - c0 : TP::REOBS_ENVS;
+                    if (fast2)
+                        reobs_spread<A, O, true>(st, cur + TP::OB, cur + TP::TG, list + c0, nc,
+                                                 obsr, pr.cap_distance, lane);
+                    else
+                        reobs_spread<A, O, false>(st, cur + TP::OB, cur + TP::TG, list + c0, nc,
+                                                  obsr, pr.cap_distance, lane);
+                    wave_sync();
+#pragma unroll
+                    for (int q = 0; q < RPL; ++q)
+                        if (row_on[q] && ((finmask >> rel[q]) & 1u) && rank[q] >= c0 &&
+                            rank[q] < c0 + nc) {
+                            const float *o = obsr + ((rank[q] - c0) * A + a) * D;
+#pragma unroll
+                            for (int j = 0; j < D; ++j) rowv[q][j] = o[j];
+                        }
+                    wave_sync();
                 }
             }
         }
@@ -1595,8 +1669,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
         g_stamps[(size_t)gw * 24 + 16] = t_entry;
         g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
         g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 19] = n_fin;
     }
 #endif
+    (void)n_fin;
 }
 
 // ------------------------------------------------------ pair-split kernel

@@ -28,16 +28,20 @@ def main():
         nb = P + 64  # >= waves of any step kernel (one env per wave at most)
         buf = torch.zeros(nb * 24, dtype=torch.int64, device="cuda")
         assert lib.marlnav_debug_stamps(buf.data_ptr()) == 0
-        acts = torch.zeros(P, A, 2, device="cuda")
-        acts[..., 0] = 0.1
-        for _ in range(5):
-            env.step(acts)
+        # bench.py's action stream (U(-0.5, 0.5) angle and acceleration)
+        g = torch.Generator(device="cuda").manual_seed(1234)
+        acts_l = [torch.stack([torch.rand(P, A, generator=g, device="cuda") - 0.5,
+                               torch.rand(P, A, generator=g, device="cuda") - 0.5], 2)
+                  for _ in range(8)]
+        acts = acts_l[0]
+        for i in range(int(os.environ.get("WARM", "5"))):
+            env.step(acts_l[i % 8])
         torch.cuda.synchronize()
         res = []
         b2b = int(os.environ.get("B2B", "1"))
         for _ in range(5):
-            for _ in range(b2b):  # back-to-back launches: keep every XCD busy
-                env.step(acts)
+            for i in range(b2b):  # back-to-back launches: keep every XCD busy
+                env.step(acts_l[i % 8])
             torch.cuda.synchronize()
             raw = buf.view(nb, 24).cpu().numpy().astype(np.int64)
             raw = raw[raw[:, 0] > 0]  # waves past the last tile record nothing
@@ -70,6 +74,18 @@ def main():
         print(cfg, "entry percentiles us:", [round(float(np.percentile(e_rel, q)), 2)
                                              for q in (0, 10, 25, 50, 75, 90, 100)])
         print(cfg, "spans", [r["span_us"] for r in res])
+        # waves that re-observed finished envs vs the rest: do they set the end?
+        reo = raw[:, 19] > 0  # tiles with a finished env (re-init + re-observe)
+        fin_t = rt[:, 7] - t0
+        for name, m in (("with_reobs", reo), ("without", ~reo)):
+            if m.any():
+                print(cfg, name, {"waves": int(m.sum()),
+                                  "chain_median_us": round(float(np.median(rt[m, 7] - entry[m])), 2),
+                                  "end_p50_us": round(float(np.percentile(fin_t[m], 50)), 2),
+                                  "end_p99_us": round(float(np.percentile(fin_t[m], 99)), 2),
+                                  "end_max_us": round(float(fin_t[m].max()), 2),
+                                  "phase_median_us": {n: round(float(np.median(ph[m, i])), 2)
+                                                      for i, n in enumerate(names)}})
         del env
 
 
