@@ -2144,6 +2144,536 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
 #endif
 }
 
+// ------------------------------------------------------- env-block kernel
+// One workgroup of A waves per block of E = 64 consecutive envs: lane l of
+// wave w owns agent w of env l. Every lane holds a row (the tile kernels
+// leave 64 - 3*20 = 4 lanes idle at A3), the agent index is wave-uniform, and
+// the per-env phase runs once per block on wave 0 with all 64 lanes busy
+// instead of on 20 of 64 lanes in every wave. Grid shape: at 65536 envs x 3
+// agents, 1024 blocks of 3 waves = 3 waves on every SIMD, where 64/3-env
+// wave tiles give 3277 waves and a fifth of the SIMDs a fourth wave (measured
+// by scripts/kstamps.py: those SIMDs set the kernel's end).
+// Rows are exchanged through LDS between block barriers (5 per step); the
+// packed observation rows are assembled in LDS and streamed out as one
+// contiguous span (a store instruction covers 1 KiB, 8 cache lines, where
+// register-row stores at a 48-byte lane stride touch 24).
+template <int A, int O>
+struct BlockPlan {
+    static constexpr int E = 64, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
+    static constexpr int NT = 64 * A;                      // threads per block
+    static constexpr int ST = 0;                           // (R, 5)
+    static constexpr int ACT = (ST + R * 5 + 3) & ~3;      // (R, 2)
+    static constexpr int OB = (ACT + R * 2 + 3) & ~3;      // (E, O, 2)
+    static constexpr int TG = (OB + E * O * 2 + 3) & ~3;   // (E, 2)
+    static constexpr int SN = (TG + E * 2 + 3) & ~3;       // (E,)
+    static constexpr int TM = (SN + E + 3) & ~3;           // (E,) bytes
+    static constexpr int FORM = (TM + E / 4 + 3) & ~3;     // 5A + 2 (native re-init)
+    static constexpr int RED = (FORM + 5 * A + 2 + 3) & ~3;  // (R, 4) reward terms
+    static constexpr int OBS = RED + 4 * R;                // (R, D) packed rows
+    static constexpr int LIST = (OBS + R * D + 3) & ~3;    // (E,) finished envs
+    static constexpr int FLG = LIST + E;                   // [0] nfin, [1 + w] wave w coords bad
+    static constexpr int FLOATS = (FLG + 1 + A + 3) & ~3;
+    static_assert(A >= 2 && A <= 16, "one wave per agent");
+};
+
+// Copy NB bytes of the block's span k into LDS by LDS-DMA from the wave
+// k % A (spans spread over the block's waves).
+template <int NB>
+__device__ __forceinline__ void block_glds(int k, int A, int w, const void *src, float *dst,
+                                           unsigned lane)
+{
+    if (k % A == w) glds_span<NB>(src, dst, lane);
+}
+
+// plain strided copy of n elements by the block's NT threads (partial block)
+template <class T>
+__device__ __forceinline__ void block_copy(const T *__restrict__ src, T *__restrict__ dst, int n,
+                                           int tid, int nt)
+{
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (int i = tid; i < n; i += nt) dst[i] = src[i];
+}
+
+// LDS span -> global span of n floats by the block's threads; 16-byte
+// vectors for the aligned head (both bases 16-byte aligned by construction)
+__device__ __forceinline__ void block_store(float *__restrict__ dst, const float *__restrict__ src,
+                                            int n, int tid, int nt)
+{
+    const int n4 = n >> 2;
+    for (int i = tid; i < n4; i += nt)
+        reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(src)[i];
+    for (int i = (n4 << 2) + tid; i < n; i += nt) dst[i] = src[i];
+}
+
+// Re-observation of the finished envs (environment.py:105) spread over the
+// block: one (row, pair) item per thread per pass, results written straight
+// into the block's packed rows. Per wave and pass, the short sqrt/division
+// sequences run when every coordinate of the pass passes coord_ok, IEEE
+// otherwise.
+template <int A, int O>
+__device__ __forceinline__ void reobs_block(const float *st, const float *ob, const float *tg,
+                                            const int *list, int nfin, float *obs_rows,
+                                            float cap, int tid, int nt)
+{
+    constexpr int NP = 1 + O + (A - 1), D = 2 + 2 * O + 2 * (A - 1);
+    const int nw = nfin * A * NP;
+    for (int base = 0; base < nw; base += nt) {
+        const int w = base + tid;
+        const bool on = w < nw;
+        const int wc = on ? w : 0;
+        const int fe = wc / (A * NP), rem = wc - fe * (A * NP);
+        const int ag = rem / NP, p = rem - ag * NP;
+        const int env = list[fe];
+        const float *s = st + 5 * (env * A + ag);
+        const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
+        const float *pt;
+        int sa, sd;
+        if (p == 0) {            // target
+            pt = tg + 2 * env;
+            sa = 0;
+            sd = 1;
+        } else if (p <= O) {     // obstacle p - 1
+            pt = ob + 2 * (env * O + p - 1);
+            sa = 1 + p;
+            sd = 1 + O + p;
+        } else {                 // other agent kx, skipping self
+            const int kx = p - O - 1;
+            pt = st + 5 * (env * A + kx + (kx >= ag ? 1 : 0));
+            sa = 2 + 2 * O + kx;
+            sd = 2 + 2 * O + (A - 1) + kx;
+        }
+        const float px = pt[0], py = pt[1];
+        const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+        bool unused = true;
+        float d, ang;
+        if (__ballot(on && !cok) == 0ull) {
+            d = pair_dist<true>(ox, oy, px, py, unused);
+            ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+        } else {
+            d = pair_dist<false>(ox, oy, px, py, unused);
+            ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+        }
+        if (on) {
+            float *o = obs_rows + (env * A + ag) * D;
+            o[sa] = ang;
+            o[sd] = d;
+        }
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void lds_row_write(float *dst, const float *row)
+{
+    if constexpr (D % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 4)
+            *reinterpret_cast<float4 *>(dst + k) = make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]);
+    } else if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 2)
+            *reinterpret_cast<float2 *>(dst + k) = make_float2(row[k], row[k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) dst[k] = row[k];
+    }
+}
+
+// Re-initialisation of the finished envs (environment.py:76-90, the sampler
+// call at :78) spread over the block: one item per thread per pass - one
+// float of a fresh candidate (reference RNG) or of the formation template,
+// or one Philox block of two obstacles (native; the same draws as
+// native_fresh_env). Writes the block's LDS state and the global obstacles /
+// target; the agent rows go out with the block's final stores.
+template <int A, int O>
+__device__ __forceinline__ void reinit_block(KArgsK *kl, float *st, float *ob, float *tg,
+                                             const float *form, const int *list, int nfin,
+                                             int64_t e0, int tid, int nt)
+{
+    float *gob = kl->a.b.obstacles;
+    float *gtg = kl->a.b.target;
+    const float *fs = kl->a.b.fresh_states;
+    if (fs) {
+        const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
+        const bool keep = (kl->p.flags & MARLNAV_FRESH_STATES_FROM_MOVED) != 0;
+        constexpr int NI = 5 * A + 2 * O + 2;
+        for (int i = tid; i < nfin * NI; i += nt) {
+            const int fe = i / NI, kk = i - fe * NI;
+            const int env = list[fe];
+            const int64_t e = e0 + env;
+            if (kk < 5 * A) {
+                if (!keep) st[5 * A * env + kk] = fs[e * A * 5 + kk];
+            } else if (kk < 5 * A + 2 * O) {
+                const int j = kk - 5 * A;
+                const float v = fo[e * O * 2 + j];
+                ob[2 * O * env + j] = v;
+                gob[e * O * 2 + j] = v;
+            } else {
+                const int j = kk - 5 * A - 2 * O;
+                const float v = ft[2 * e + j];
+                tg[2 * env + j] = v;
+                gtg[2 * e + j] = v;
+            }
+        }
+        return;
+    }
+    constexpr int NB = (O + 1) / 2, NI = 5 * A + 2 + NB;
+    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
+    const int64_t eoff = kl->a.env_offset;
+    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
+    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
+    for (int i = tid; i < nfin * NI; i += nt) {
+        const int fe = i / NI, kk = i - fe * NI;
+        const int env = list[fe];
+        const int64_t e = e0 + env;
+        if (kk < 5 * A) {
+            st[5 * A * env + kk] = form[kk];
+        } else if (kk < 5 * A + 2) {
+            const int j = kk - 5 * A;
+            tg[2 * env + j] = form[kk];
+            gtg[2 * e + j] = form[kk];
+        } else {
+            const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
+            const uint64_t gid = (uint64_t)(eoff + e);
+            uint32_t c[4] = {(uint32_t)jb, (uint32_t)sidx, (uint32_t)gid,
+                             (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
+            philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+            const int j = 2 * jb;
+            float *o = ob + 2 * O * env + 2 * j;
+            float *g = gob + e * O * 2 + 2 * j;
+            o[0] = g[0] = rx * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+            o[1] = g[1] = ry * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
+            if (j + 1 < O) {
+                o[2] = g[2] = rx * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+                o[3] = g[3] = ry * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
+            }
+        }
+    }
+}
+
+#ifndef MARLNAV_BLK_EARLY  // 1: stream rows/states out before the per-env phase
+#define MARLNAV_BLK_EARLY 0
+#endif
+#ifndef MARLNAV_BLK_SPREAD  // 1: re-init finished envs spread over the block
+#define MARLNAV_BLK_SPREAD 1
+#endif
+constexpr bool kBlkEarly = MARLNAV_BLK_EARLY != 0;
+constexpr bool kBlkSpread = MARLNAV_BLK_SPREAD != 0;
+
+// Phases (one block barrier after each): stage | move + coordinate check
+// (moved states start streaming out) | observe into LDS rows | rows stream
+// out while wave 0 runs the per-env phase | re-init, re-observe and re-store
+// the finished envs only (none in most blocks).
+template <int A, int O, bool OBS_ONLY, bool NOISY>
+__global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
+{
+    using BP = BlockPlan<A, O>;
+    constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
+    (void)k;  // read through kargs_late()
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+#if MARLNAV_STAMPS
+    unsigned long long t_entry;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
+#endif
+    const int tid = (int)threadIdx.x;
+    const unsigned lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // agent of this wave
+    const int64_t blk = blockIdx.x;
+    const int64_t gw = blk * A + w;  // stamps slot
+    KArgsK *K = kargs_late();
+    const int64_t P = K->a.P;
+    if (blk >= K->a.ntiles) return;
+    STAMP(0);
+    const StepPtrs b = load_ptrs(K);
+    float *st = lds + BP::ST;
+    const int64_t e0 = blk * E;
+    const int ne = (int)((P - e0) < E ? (P - e0) : E);
+    const bool full = ne == E;
+
+    // ---- stage the block (spans spread over the waves)
+    if (full) {
+        block_glds<R * 20>(0, A, w, b.states + e0 * (A * 5), st, lane);
+        if (!OBS_ONLY) block_glds<R * 8>(1, A, w, b.actions + e0 * (A * 2), lds + BP::ACT, lane);
+        block_glds<E * O * 8>(2, A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
+        block_glds<E * 8>(3, A, w, b.target + e0 * 2, lds + BP::TG, lane);
+        if (!OBS_ONLY) {
+            block_glds<E * 4>(4, A, w, b.step_num + e0, lds + BP::SN, lane);
+            block_glds<E>(5, A, w, b.terminates + e0, lds + BP::TM, lane);
+            if (b.formation)
+                block_glds<(5 * A + 2) * 4>(6, A, w, b.formation, lds + BP::FORM, lane);
+        }
+    } else {
+        const int nr = ne * A;
+        block_copy(b.states + e0 * (A * 5), st, nr * 5, tid, NT);
+        if (!OBS_ONLY) block_copy(b.actions + e0 * (A * 2), lds + BP::ACT, nr * 2, tid, NT);
+        block_copy(b.obstacles + e0 * (O * 2), lds + BP::OB, ne * O * 2, tid, NT);
+        block_copy(b.target + e0 * 2, lds + BP::TG, ne * 2, tid, NT);
+        if (!OBS_ONLY) {
+            block_copy(b.step_num + e0, lds + BP::SN, ne, tid, NT);
+            block_copy(b.terminates + e0, reinterpret_cast<uint8_t *>(lds + BP::TM), ne, tid, NT);
+            if (b.formation) block_copy(b.formation, lds + BP::FORM, 5 * A + 2, tid, NT);
+        }
+    }
+    const MarlnavParams pr = load_params(K);
+    const int l = (int)lane;  // env of this lane within the block
+    const int r = l * A + w;  // row of this lane
+    const bool row_on = l < ne;
+    const int nrow = ne * A;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+    __syncthreads();
+    STAMP(1);
+
+    // ---- _move_agents (environment.py:113-123), own row in registers
+    float ox, oy, dx, dy;
+    {
+        const float *s = st + 5 * r;
+        ox = s[0];
+        oy = s[1];
+        dx = s[2];
+        dy = s[3];
+    }
+    if (!OBS_ONLY) {
+        const float2 act = reinterpret_cast<const float2 *>(lds + BP::ACT)[r];
+        float a0 = act.x, a1 = act.y;
+        if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
+            KArgsK *kl = kargs_late();
+            a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
+            a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
+        }
+        float sn, c;
+        sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+        const float ndx = c * dx + (-sn) * dy;
+        const float ndy = sn * dx + c * dy;
+        float *s = st + 5 * r;
+        const float v = clamp_t(s[4] + clamp_t(a1, pr.min_accel, pr.max_accel), pr.min_speed,
+                                pr.max_speed);
+        ox = ox + ndx * v;
+        oy = oy + ndy * v;
+        dx = ndx;
+        dy = ndy;
+        if (row_on) {
+            s[0] = ox;
+            s[1] = oy;
+            s[2] = dx;
+            s[3] = dy;
+            s[4] = v;
+        }
+    }
+    // block-uniform choice of the pair math: the short sqrt / shared-
+    // reciprocal division (equal to IEEE there) when every coordinate of the
+    // block passes coord_ok, IEEE otherwise
+    {
+        bool cok = !row_on || (coord_ok(ox) && coord_ok(oy));
+        constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
+        static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
+        for (int i = tid; i < NC; i += NT) {
+            const bool used = full || (i < E * O * 2 ? i / (O * 2) < ne : (i - E * O * 2) / 2 < ne);
+            cok = cok && (!used || coord_ok(lds[BP::OB + i]));
+        }
+        const bool bad = __ballot(!cok) != 0ull;
+        if (lane == 0) reinterpret_cast<int *>(lds + BP::FLG)[1 + w] = bad ? 1 : 0;
+    }
+    __syncthreads();
+    STAMP(2);
+    // the moved states are final except in finished envs (re-stored below)
+    if (kBlkEarly && !OBS_ONLY) block_store(in_sgpr(b.states + e0 * (A * 5)), st, nrow * 5, tid, NT);
+    bool fast = full;
+#pragma unroll
+    for (int q = 0; q < A; ++q) fast = fast && reinterpret_cast<const int *>(lds + BP::FLG)[1 + q] == 0;
+
+    // ---- observations of the moved state + reward terms (:99-100)
+    float4 *red = reinterpret_cast<float4 *>(lds + BP::RED);
+    float *obs_rows = lds + BP::OBS;
+    if (!(MARLNAV_ABLATE & 16) && row_on) {
+        float rowv[D];
+        RowOut ro;
+        bool unused = true;
+        if (__builtin_expect(fast, 1))
+            ro = observe_row_own<A, O, !OBS_ONLY, true>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
+                                                        lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
+                                                        rowv, pr, unused);
+        else
+            ro = observe_row_own<A, O, !OBS_ONLY, false>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
+                                                         lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
+                                                         rowv, pr, unused);
+        lds_row_write<D>(obs_rows + r * D, rowv);
+        if (!OBS_ONLY) red[r] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
+    }
+    __syncthreads();
+    STAMP(3);
+    // every row streams out now; the finished envs' rows are re-stored below
+    float *gobs = in_sgpr(b.obs + e0 * (A * D));
+    if (kBlkEarly || OBS_ONLY) block_store(gobs, obs_rows, nrow * D, tid, NT);
+    const bool norm = !OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM);
+    if (norm && kBlkEarly) {
+        KArgsK *kl = kargs_late();
+        const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
+        float *gn = kl->a.b.obs_norm + e0 * (A * D);
+        for (int i = tid; i < nrow * D; i += NT) {
+            const int kk = i % D;
+            gn[i] = (obs_rows[i] - mean[kk]) / scale[kk];
+        }
+    }
+
+    if (!OBS_ONLY) {
+        int *list = reinterpret_cast<int *>(lds + BP::LIST);
+        int *flg = reinterpret_cast<int *>(lds + BP::FLG);
+        // ---- per-env reductions, terminal logic (wave 0, one lane per env)
+        if (w == 0) {
+            const bool env_on = l < ne;
+            bool fin = false, tr_l = false, co_l = false, ta_l = false;
+            if (env_on) {
+                const int64_t e = e0 + l;
+                float4 rr[A];
+#pragma unroll
+                for (int i = 0; i < A; ++i) rr[i] = red[A * l + i];
+                unsigned any_col = 0u, all_in = 1u;
+#pragma unroll
+                for (int i = 0; i < A; ++i) {
+                    const unsigned f = __float_as_uint(rr[i].z);
+                    any_col |= f & 1u;
+                    all_in &= (f >> 1) & 1u;
+                }
+                float rv[A];
+#pragma unroll
+                for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
+                const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
+                b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
+
+                float step_num = lds[BP::SN + l] + 1.0f;           // :96
+                const bool truncated = step_num > pr.trunc_after;  // :97
+                const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
+                const bool terminated = any_col || term_old;       // :213-214
+                b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
+                b.terminated[e] = (uint8_t)terminated;
+                b.truncated[e] = (uint8_t)truncated;
+                fin = truncated || terminated;                     // :102-104
+                if ((NOISY || !kBlkSpread) && fin) {  // serial re-init per env
+                    KArgsK *kl = kargs_late();
+                    if (!NOISY && kl->a.b.fresh_states) {
+                        float *s5 = st + 5 * A * l;
+                        float *obl = lds + BP::OB + 2 * O * l;
+                        float *tgl = lds + BP::TG + 2 * l;
+                        const float *fs = kl->a.b.fresh_states;
+                        const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
+                        if (!(kl->p.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
+                            for (int i = 0; i < 5 * A; ++i) s5[i] = fs[e * A * 5 + i];
+                        for (int i = 0; i < 2 * O; ++i) obl[i] = fo[e * O * 2 + i];
+                        tgl[0] = ft[2 * e];
+                        tgl[1] = ft[2 * e + 1];
+                        for (int i = 0; i < 2 * O; ++i) kl->a.b.obstacles[e * O * 2 + i] = obl[i];
+                        kl->a.b.target[2 * e] = tgl[0];
+                        kl->a.b.target[2 * e + 1] = tgl[1];
+                    } else {
+                        MarlnavParams p;  // the fields the re-init reads
+                        p.obs_range_x = kl->p.obs_range_x;
+                        p.obs_mean_x = kl->p.obs_mean_x;
+                        p.obs_range_y = kl->p.obs_range_y;
+                        p.obs_mean_y = kl->p.obs_mean_y;
+                        p.ags_dist = kl->p.ags_dist;
+                        p.noise_std = kl->p.noise_std;
+                        p.angle_range = kl->p.angle_range;
+                        p.flags = kl->p.flags;
+                        p.seed = kl->p.seed;
+                        float *obl = lds + BP::OB + 2 * O * l;
+                        float *tgl = lds + BP::TG + 2 * l;
+                        native_fresh_env<NOISY>(A, O, p, lds + BP::FORM,
+                                                (uint64_t)(kl->a.env_offset + e), kl->a.step_idx,
+                                                st + 5 * A * l, obl, tgl);
+                        float *gob = kl->a.b.obstacles;
+                        for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
+                        kl->a.b.target[2 * e] = tgl[0];
+                        kl->a.b.target[2 * e + 1] = tgl[1];
+                    }
+                }
+                b.step_num[e] = fin ? 0.0f : step_num;
+                tr_l = truncated;
+                co_l = any_col;
+                ta_l = all_in;
+            }
+            const uint64_t finmask = __ballot(fin);
+            if (fin)
+                list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] = l;
+            const unsigned c_trunc = __popcll(__ballot(tr_l));
+            const unsigned c_col = __popcll(__ballot(co_l));
+            const unsigned c_tar = __popcll(__ballot(ta_l));
+            if (lane == 0) {
+                flg[0] = (int)__popcll(finmask);
+                if (c_trunc | c_col | c_tar) {
+                    KArgsK *kl = kargs_late();
+                    uint64_t *cnt = kl->a.b.counters;
+                    const int64_t slots = kl->a.waves;
+                    if (cnt) {
+                        const int64_t sl = blk % slots;
+                        if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
+                        if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + sl], (unsigned long long)c_col);
+                        if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        STAMP(4);
+        const int nfin = flg[0];
+        if (nfin) {
+            // ---- masked re-init (:104) and observations of the re-initialised
+            // envs (:105), then their rows and states go out again
+            if (!NOISY && kBlkSpread) {
+                reinit_block<A, O>(kargs_late(), st, lds + BP::OB, lds + BP::TG, lds + BP::FORM,
+                                   list, nfin, e0, tid, NT);
+                __syncthreads();
+            }
+            reobs_block<A, O>(st, lds + BP::OB, lds + BP::TG, list, nfin, obs_rows,
+                              pr.cap_distance, tid, NT);
+            __syncthreads();
+            constexpr int NI = A * D + 5 * A;
+            float *gst = in_sgpr(b.states + e0 * (A * 5));
+            for (int i = tid; kBlkEarly && i < nfin * NI; i += NT) {
+                const int fe = i / NI, kk = i - fe * NI;
+                const int env = list[fe];
+                if (kk < A * D) gobs[env * (A * D) + kk] = obs_rows[env * (A * D) + kk];
+                else gst[env * (A * 5) + kk - A * D] = st[env * (A * 5) + kk - A * D];
+            }
+            if (norm && kBlkEarly) {
+                KArgsK *kl = kargs_late();
+                const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
+                float *gn = kl->a.b.obs_norm + e0 * (A * D);
+                for (int i = tid; i < nfin * A * D; i += NT) {
+                    const int fe = i / (A * D), kk = i - fe * (A * D);
+                    const int o = list[fe] * (A * D) + kk;
+                    gn[o] = (obs_rows[o] - mean[kk % D]) / scale[kk % D];
+                }
+            }
+        }
+    }
+    STAMP(5);
+    if (!kBlkEarly && !OBS_ONLY) {  // ---- stream the block out
+        block_store(gobs, obs_rows, nrow * D, tid, NT);
+        if (norm) {
+            KArgsK *kl = kargs_late();
+            const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
+            float *gn = kl->a.b.obs_norm + e0 * (A * D);
+            for (int i = tid; i < nrow * D; i += NT) {
+                const int kk = i % D;
+                gn[i] = (obs_rows[i] - mean[kk]) / scale[kk];
+            }
+        }
+        block_store(in_sgpr(b.states + e0 * (A * 5)), st, nrow * 5, tid, NT);
+    }
+    STAMP(6);
+#if MARLNAV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(7);
+    if (lane == 0) {
+        g_stamps[(size_t)gw * 24 + 16] = t_entry;
+        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 19] = OBS_ONLY ? 0u : (unsigned)reinterpret_cast<const int *>(lds + BP::FLG)[0];
+    }
+#endif
+    (void)gw;
+}
+
 // ----------------------------------------------------- native reinit kernel
 __global__ void reinit_all_kernel(int64_t P, int A, int S, int64_t env_offset, uint64_t sidx,
                                   MarlnavParams pr, const float *__restrict__ formation,
@@ -2376,6 +2906,61 @@ int launch_split(const SplitVariant &v, TileFn fn, const StepArgs &args, const M
     return 0;
 }
 
+// env-block kernels (block_kernel) for these shapes; MARLNAV_BLOCK=0 turns
+// them off (A/B timing against the tile kernels)
+struct BlockVariant {
+    int A, O;
+    TileFn step, obs, noisy;
+    size_t lds;
+};
+
+#define MARLNAV_BLOCK_VARIANT(A, O)                                                    \
+    {A, O, block_kernel<A, O, false, false>, block_kernel<A, O, true, false>,          \
+     block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4}
+const BlockVariant kBlockVariants[] = {
+    MARLNAV_BLOCK_VARIANT(3, 3),
+    MARLNAV_BLOCK_VARIANT(3, 8),
+    MARLNAV_BLOCK_VARIANT(3, 1),
+    MARLNAV_BLOCK_VARIANT(2, 1),
+};
+#undef MARLNAV_BLOCK_VARIANT
+
+const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only)
+{
+    static const int forced = [] {
+        const char *v = getenv("MARLNAV_BLOCK");
+        return v ? (int)strtol(v, nullptr, 10) : -1;
+    }();
+    if (forced == 0 || d->obstacle_stride != d->num_obstacles) return nullptr;
+    const BlockVariant *v = nullptr;
+    for (const BlockVariant &x : kBlockVariants)
+        if (x.A == d->num_agents && x.O == d->num_obstacles) v = &x;
+    if (!v) return nullptr;
+    if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
+        !aligned(b.obs, 16))
+        return nullptr;
+    if (!obs_only && (!aligned(b.actions, 16) || !aligned(b.step_num, 16) ||
+                      !aligned(b.terminates, 16) || (b.formation && !aligned(b.formation, 16))))
+        return nullptr;
+    return v;
+}
+
+int launch_block(const BlockVariant &v, TileFn fn, const StepArgs &args, const MarlnavParams &pr,
+                 void *stream, const char *what)
+{
+    KArgs ka;
+    ka.a = args;
+    ka.p = pr;
+    ka.a.W = BlockPlan<3, 3>::E;
+    ka.a.ntiles = (args.P + ka.a.W - 1) / ka.a.W;
+    void *kargs[] = {&ka};
+    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)ka.a.ntiles),
+                                   dim3(64 * v.A), kargs, v.lds, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+    return 0;
+}
+
 int launch_tile(TileFn fn, size_t lds, int rpl, const Launch &L, const StepArgs &args,
                 const MarlnavParams &pr, void *stream, const char *what)
 {
@@ -2483,6 +3068,8 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavSte
     const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
     if (const SplitVariant *v = select_split(d, *b, false))
         return launch_split(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
+    if (const BlockVariant *v = select_block(d, *b, false))
+        return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
     if (const TilePair *t = select_tile(d, *b, false)) {
         const int r = pick_rpl(d->num_parallel, d->num_agents);
         const TileSet &ts = t->rpl[r - 1];
@@ -2510,6 +3097,8 @@ int marlnav_observe(const MarlnavDims *d, const float *states, const float *obst
     pr.cap_distance = 0.1f;  // environment.py:65
     if (const SplitVariant *v = select_split(d, args.b, true))
         return launch_split(*v, v->obs, args, pr, stream, "marlnav_observe");
+    if (const BlockVariant *v = select_block(d, args.b, true))
+        return launch_block(*v, v->obs, args, pr, stream, "marlnav_observe");
     if (const TilePair *t = select_tile(d, args.b, true)) {
         const int r = pick_rpl(d->num_parallel, d->num_agents);
         return launch_tile(t->rpl[r - 1].obs, t->rpl[r - 1].lds, r, L, args, pr, stream,

@@ -74,6 +74,25 @@ def main():
         print(cfg, "entry percentiles us:", [round(float(np.percentile(e_rel, q)), 2)
                                              for q in (0, 10, 25, 50, 75, 90, 100)])
         print(cfg, "spans", [r["span_us"] for r in res])
+        # SIMD load balance: waves per SIMD (HW_ID simd/cu/sh/se + XCC_ID) and
+        # the end time of waves by their SIMD's wave count
+        hw = raw[:, 17]
+        key = ((xcc.astype(np.int64) << 16) | ((hw >> 13) & 7) << 12 | ((hw >> 12) & 1) << 8
+               | ((hw >> 8) & 15) << 4 | ((hw >> 4) & 3))
+        uk, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+        per_wave_cnt = cnt[inv]
+        cu_key = key >> 4
+        ucu, cu_cnt = np.unique(cu_key, return_counts=True)
+        print(cfg, "simds used", len(uk), "waves/simd histogram",
+              {int(k): int(v) for k, v in zip(*np.unique(cnt, return_counts=True))},
+              "cus used", len(ucu), "waves/cu histogram",
+              {int(k): int(v) for k, v in zip(*np.unique(cu_cnt, return_counts=True))})
+        fin_all = rt[:, 7] - t0
+        for c in np.unique(per_wave_cnt):
+            m = per_wave_cnt == c
+            print(cfg, f"waves on {int(c)}-wave SIMDs: n={int(m.sum())} end p50/p90/max us",
+                  [round(float(np.percentile(fin_all[m], q)), 2) for q in (50, 90, 100)],
+                  "chain p50", round(float(np.median(rt[m, 7] - entry[m])), 2))
         # waves that re-observed finished envs vs the rest: do they set the end?
         reo = raw[:, 19] > 0  # tiles with a finished env (re-init + re-observe)
         fin_t = rt[:, 7] - t0
