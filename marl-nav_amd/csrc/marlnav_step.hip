@@ -2350,6 +2350,119 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, float *st, float *ob, f
     }
 }
 
+// Native (non-noisy) re-init and re-observation of the finished envs in ONE
+// pass over the block: a fresh env's agent rows and target are the formation
+// template and its obstacles are Philox draws (the same as native_fresh_env),
+// so each observation item computes its own inputs instead of waiting for a
+// re-init pass and a barrier. Items per finished env: A*(1+O+A-1) pairs
+// (written into the packed rows), 5A+2 template floats and ceil(O/2) Philox
+// blocks (written to the LDS state and the global obstacles/target).
+template <int A, int O>
+__device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, float *st, float *ob, float *tg,
+                                                    const float *form, const int *list, int nfin,
+                                                    float *obs_rows, float cap, int64_t e0,
+                                                    int tid, int nt)
+{
+    constexpr int NP = 1 + O + (A - 1), D = 2 + 2 * O + 2 * (A - 1), NB = (O + 1) / 2;
+    constexpr int NPAIR = A * NP, NI = NPAIR + 5 * A + 2 + NB;
+    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
+    const int64_t eoff = kl->a.env_offset;
+    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
+    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
+    float *gob = kl->a.b.obstacles;
+    float *gtg = kl->a.b.target;
+    const int n = nfin * NI;
+    for (int base = 0; base < n; base += nt) {
+        const int i = base + tid;
+        const bool on = i < n;
+        const int ic = on ? i : 0;
+        const int fe = ic / NI, kk = ic - fe * NI;
+        const int env = list[fe];
+        const int64_t e = e0 + env;
+        const uint64_t gid = (uint64_t)(eoff + e);
+        const bool pair = kk < NPAIR;
+        // Philox block: obstacle pair items (the block of their obstacle) and
+        // obstacle store items
+        int jb = -1;
+        int ag = 0, p = 0;
+        if (pair) {
+            ag = kk / NP;
+            p = kk - ag * NP;
+            if (p >= 1 && p <= O) jb = (p - 1) >> 1;
+        } else if (kk >= NPAIR + 5 * A + 2) {
+            jb = kk - (NPAIR + 5 * A + 2);
+        }
+        uint32_t c[4] = {0u, 0u, 0u, 0u};
+        if (jb >= 0) {
+            c[0] = (uint32_t)jb;
+            c[1] = (uint32_t)sidx;
+            c[2] = (uint32_t)gid;
+            c[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
+            philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        }
+        if (pair) {
+            const float *s = form + 5 * ag;
+            const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
+            float px, py;
+            int sa, sd;
+            if (p == 0) {            // target
+                px = form[5 * A];
+                py = form[5 * A + 1];
+                sa = 0;
+                sd = 1;
+            } else if (p <= O) {     // obstacle p - 1: components of its Philox block
+                const bool hi = ((p - 1) & 1) != 0;
+                const uint32_t ux = hi ? c[2] : c[0], uy = hi ? c[3] : c[1];
+                px = rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx;
+                py = ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my;
+                sa = 1 + p;
+                sd = 1 + O + p;
+            } else {                 // other agent kx, skipping self
+                const int kx = p - O - 1;
+                const float *q = form + 5 * (kx + (kx >= ag ? 1 : 0));
+                px = q[0];
+                py = q[1];
+                sa = 2 + 2 * O + kx;
+                sd = 2 + 2 * O + (A - 1) + kx;
+            }
+            const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+            bool unused = true;
+            float d, ang;
+            if (__ballot(on && !cok) == 0ull) {
+                d = pair_dist<true>(ox, oy, px, py, unused);
+                ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+            } else {
+                d = pair_dist<false>(ox, oy, px, py, unused);
+                ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+            }
+            if (on) {
+                float *o = obs_rows + (env * A + ag) * D;
+                o[sa] = ang;
+                o[sd] = d;
+            }
+        } else if (on) {
+            const int k2 = kk - NPAIR;
+            if (k2 < 5 * A) {
+                st[5 * A * env + k2] = form[k2];
+            } else if (k2 < 5 * A + 2) {
+                const int j = k2 - 5 * A;
+                tg[2 * env + j] = form[k2];
+                gtg[2 * e + j] = form[k2];
+            } else {
+                const int j = 2 * jb;
+                float *o = ob + 2 * O * env + 2 * j;
+                float *g = gob + e * O * 2 + 2 * j;
+                o[0] = g[0] = rx * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+                o[1] = g[1] = ry * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
+                if (j + 1 < O) {
+                    o[2] = g[2] = rx * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+                    o[3] = g[3] = ry * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
+                }
+            }
+        }
+    }
+}
+
 #ifndef MARLNAV_BLK_EARLY  // 1: stream rows/states out before the per-env phase
 #define MARLNAV_BLK_EARLY 0
 #endif
@@ -2465,9 +2578,14 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
         bool cok = !row_on || (coord_ok(ox) && coord_ok(oy));
         constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
         static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
-        for (int i = tid; i < NC; i += NT) {
-            const bool used = full || (i < E * O * 2 ? i / (O * 2) < ne : (i - E * O * 2) / 2 < ne);
-            cok = cok && (!used || coord_ok(lds[BP::OB + i]));
+#pragma unroll
+        for (int k2 = 0; k2 * NT < NC; ++k2) {
+            const int i = tid + k2 * NT;
+            if ((k2 + 1) * NT <= NC || i < NC) {
+                const bool used =
+                    full || (i < E * O * 2 ? i / (O * 2) < ne : (i - E * O * 2) / 2 < ne);
+                cok = cok && (!used || coord_ok(lds[BP::OB + i]));
+            }
         }
         const bool bad = __ballot(!cok) != 0ull;
         if (lane == 0) reinterpret_cast<int *>(lds + BP::FLG)[1 + w] = bad ? 1 : 0;
@@ -2618,13 +2736,19 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
         if (nfin) {
             // ---- masked re-init (:104) and observations of the re-initialised
             // envs (:105), then their rows and states go out again
-            if (!NOISY && kBlkSpread) {
-                reinit_block<A, O>(kargs_late(), st, lds + BP::OB, lds + BP::TG, lds + BP::FORM,
-                                   list, nfin, e0, tid, NT);
-                __syncthreads();
+            KArgsK *kl = kargs_late();
+            if (!NOISY && kBlkSpread && !kl->a.b.fresh_states) {
+                reinit_reobs_native<A, O>(kl, st, lds + BP::OB, lds + BP::TG, lds + BP::FORM,
+                                          list, nfin, obs_rows, pr.cap_distance, e0, tid, NT);
+            } else {
+                if (!NOISY && kBlkSpread) {
+                    reinit_block<A, O>(kl, st, lds + BP::OB, lds + BP::TG, lds + BP::FORM, list,
+                                       nfin, e0, tid, NT);
+                    __syncthreads();
+                }
+                reobs_block<A, O>(st, lds + BP::OB, lds + BP::TG, list, nfin, obs_rows,
+                                  pr.cap_distance, tid, NT);
             }
-            reobs_block<A, O>(st, lds + BP::OB, lds + BP::TG, list, nfin, obs_rows,
-                              pr.cap_distance, tid, NT);
             __syncthreads();
             constexpr int NI = A * D + 5 * A;
             float *gst = in_sgpr(b.states + e0 * (A * 5));
