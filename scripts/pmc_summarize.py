@@ -2,11 +2,21 @@
 import collections, csv, glob, json, os, sys
 out, cfg = sys.argv[1], sys.argv[2]
 acc = collections.defaultdict(list)
+STEP_KERNELS = ("wave_kernel", "tile_kernel", "split_kernel", "block_kernel")
+
+
+def is_step(name):
+    """A step launch (not the observe-only instantiation: OBS_ONLY is template arg 3)."""
+    if not any(k in name for k in STEP_KERNELS):
+        return False
+    args = name[name.index("<") + 1:name.index(">")].split(",")
+    return len(args) >= 3 and args[2].strip() == "false"
+
 dur = []
 for f in sorted(glob.glob(os.path.join(out, "p*", "run_counter_collection.csv"))):
     per = collections.defaultdict(dict)
     for r in csv.DictReader(open(f)):
-        if ("wave_kernel" not in r["Kernel_Name"] and "tile_kernel" not in r["Kernel_Name"]) or "true" in r["Kernel_Name"].split(",")[2]:
+        if not is_step(r["Kernel_Name"]):
             continue
         per[r["Counter_Name"]][r["Dispatch_Id"]] = per[r["Counter_Name"]].get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     for k, v in per.items():
@@ -15,7 +25,7 @@ for f in sorted(glob.glob(os.path.join(out, "p*", "run_counter_collection.csv"))
             acc[k].append(sum(vals) / len(vals))
 for f in glob.glob(os.path.join(out, "p*", "run_kernel_trace.csv")):
     for r in csv.DictReader(open(f)):
-        if ("wave_kernel" in r["Kernel_Name"] or "tile_kernel" in r["Kernel_Name"]) and "false, false" in r["Kernel_Name"]:
+        if is_step(r["Kernel_Name"]):
             dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 res = {k: sum(v) / len(v) for k, v in acc.items()}
 dur.sort()
