@@ -480,3 +480,69 @@ def test_extreme_coordinates_take_the_exact_path(pkg, P, A, O):
         assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, where=where)
         s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))
+
+
+@pytest.mark.parametrize("P,A,O", [(20000 + 13, 3, 3), (8192 + 5, 3, 8), (300, 3, 3)])
+def test_reference_rng_fresh_candidates_bit_exact_vs_oracle(pkg, P, A, O):
+    """rng='reference' at block-kernel sizes (and one split-kernel size):
+    finished envs take the host's fresh candidates (environment.py:76-90
+    with the sampler call at :78); episodes of 3 steps so whole blocks finish
+    together; the last block is ragged. Bit-exact vs the oracle."""
+    g = torch.Generator().manual_seed(P * 7 + O)
+    env = make_env(pkg, P, A, O, episode_len=3, rng="reference", noise_device="cpu",
+                   factors=dict(risk_factor=2., bond_factor=5.))
+    dm, pr = oracle_params(env)
+    st, ob, tg = (np_(x).copy() for x in (env.states, env.obstacles, env.target))
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    tot = np.zeros(3, np.int64)
+    for k in range(7):
+        fs = (torch.rand(P, A, 5, generator=g) * 900.0).numpy()
+        fo = (torch.rand(P, O, 2, generator=g) * 700.0).numpy()
+        ft = (torch.rand(P, 1, 2, generator=g) * 1400.0).numpy()
+        fresh = (fs, fo, ft)
+        env._init_sampler = lambda fr=fresh: tuple(torch.from_numpy(x) for x in fr)
+        acts = ((torch.rand(P, A, 2, generator=g) - 0.5) * 0.9).numpy()
+        exp = orc.step(dm, pr, st, ob, tg, sn, te, acts, fresh=fresh)
+        obs, rew, term, trunc = env.step(torch.from_numpy(acts).to(DEV))
+        where = f"P{P} A{A} O{O} step {k + 1}"
+        for name, got in (("states", env.states), ("obstacles", env.obstacles),
+                          ("target", env.target), ("step_num", env._step_num),
+                          ("terminates", env._terminates), ("terminated", term),
+                          ("truncated", trunc), ("reward", rew)):
+            np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
+        fg, fo_ = orc.split_obs(np_(obs._packed), A, O), orc.split_obs(exp["obs"], A, O)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, where=where)
+        st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
+                                               "terminates"))
+        tot += exp["counters"].astype(np.int64)
+    assert tot[0] >= P  # every env truncated at least once
+    assert [env._num_trunc, env._num_col, env._num_tar] == tot.tolist()
+
+
+@pytest.mark.parametrize("P,A,O", [(16384 + 9, 3, 3), (1000, 3, 8), (512, 16, 32)])
+def test_native_noisy_agents_bit_exact_vs_oracle(pkg, P, A, O):
+    """Native re-init with noisy agent positions and headings
+    (TriangleIntitializer noisy_ags, utils.py:350-368): the NOISY kernel
+    instantiations (block, split and generic) equal the oracle bit for bit."""
+    g = torch.Generator().manual_seed(P + 11 * O)
+    env = make_env(pkg, P, A, O, episode_len=3, seed=7, noisy_ags=True)
+    dm, pr = oracle_params(env)
+    form = np_(env._formation)
+    st, ob, tg = orc.reinit_all(dm, pr, form, 0)
+    np.testing.assert_array_equal(np_(env.states), st)
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    for k in range(5):
+        acts = ((torch.rand(P, A, 2, generator=g) - 0.5) * 0.8).numpy()
+        exp = orc.step(dm, pr, st, ob, tg, sn, te, acts, formation=form, step_idx=k + 1)
+        obs, rew, term, trunc = env.step(torch.from_numpy(acts).to(DEV))
+        where = f"P{P} A{A} O{O} step {k + 1}"
+        for name, got in (("states", env.states), ("obstacles", env.obstacles),
+                          ("target", env.target), ("step_num", env._step_num),
+                          ("reward", rew), ("terminated", term)):
+            np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
+        fg, fo_ = orc.split_obs(np_(obs._packed), A, O), orc.split_obs(exp["obs"], A, O)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, where=where)
+        st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
+                                               "terminates"))
