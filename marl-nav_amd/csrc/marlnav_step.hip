@@ -1684,6 +1684,358 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
 // and counts are OR/sum-reduced across the LPR lanes with DPP / swizzles;
 // the row's bond terms (environment.py:264-269) are evaluated by the lanes
 // that own the distances and summed by the row leader in torch's order.
+// LDS row stride of the split kernel's packed observation rows: D padded
+// (keeping 16-byte row alignment when D % 4 == 0) so that the LPR lanes of
+// each of the 32/LPR rows in a ds_write_b32 lane group hit distinct banks
+// ((a/4) mod 32, MI355X_MICROARCH.md §LDS). At A16/O32 (D = 96) unpadded rows
+// are 8-way conflicted: every row starts on bank 0.
+__host__ __device__ constexpr int split_conflicts(int s, int LPR, int rows)
+{
+    int worst = 0;
+    for (int b = 0; b < 32; ++b) {
+        int n = 0;
+        for (int l = 0; l < 32; ++l) {
+            const int r = l / LPR, q = l % LPR;
+            if (r < rows && (r * s + q) % 32 == b) ++n;
+        }
+        worst = n > worst ? n : worst;
+    }
+    return worst;
+}
+
+__host__ __device__ constexpr int split_row_stride(int D, int LPR, int rows)
+{
+    if (D % 4 != 0) return D;  // rows stored with 4/8-byte pieces: keep them dense
+    int best = D, bc = split_conflicts(D, LPR, rows);
+    for (int s = D + 4; s <= D + 32; s += 4) {
+        const int c = split_conflicts(s, LPR, rows);
+        if (c < bc) {
+            best = s;
+            bc = c;
+        }
+    }
+    return best;
+}
+
+// ------------------------------------- workgroup-spread re-init / re-observe
+// Where the block-spread re-init / re-observation below finds an env of the
+// workgroup: `c` is an env code from the finished-env list. BlockEnvs: the
+// env-block kernel's block-wide arrays (code = env within the block);
+// SplitEnvs: the pair-split kernel's wave-private tiles (code = wave * EPW +
+// env within the wave's tile, the tiles of a workgroup being consecutive).
+template <int A, int O, int RS>
+struct BlockEnvs {
+    float *st, *ob, *tg, *rows;
+    int64_t e0;
+    __device__ float *state(int c) const { return st + 5 * A * c; }
+    __device__ float *obst(int c) const { return ob + 2 * O * c; }
+    __device__ float *targ(int c) const { return tg + 2 * c; }
+    __device__ float *row(int c, int ag) const { return rows + (c * A + ag) * RS; }
+    __device__ int64_t env(int c) const { return e0 + c; }
+};
+
+template <int A, int O, int EPW, int FLOATS, int ST, int OB, int TG, int OBS, int RS>
+struct SplitEnvs {
+    float *lds;
+    int64_t e0;
+    __device__ float *wave(int c) const { return lds + (c / EPW) * FLOATS; }
+    __device__ float *state(int c) const { return wave(c) + ST + 5 * A * (c % EPW); }
+    __device__ float *obst(int c) const { return wave(c) + OB + 2 * O * (c % EPW); }
+    __device__ float *targ(int c) const { return wave(c) + TG + 2 * (c % EPW); }
+    __device__ float *row(int c, int ag) const { return wave(c) + OBS + ((c % EPW) * A + ag) * RS; }
+    __device__ int64_t env(int c) const { return e0 + c; }
+};
+
+// Re-observation of the finished envs (environment.py:105) spread over the
+// workgroup: one (row, pair) item per thread per pass, results written
+// straight into the packed rows. Per wave and pass, the short sqrt/division
+// sequences run when every coordinate of the pass passes coord_ok, IEEE
+// otherwise.
+template <int A, int O, class Envs, class List>
+__device__ __forceinline__ void reobs_block(const Envs &ev, const List &list, int nfin, float cap,
+                                            int tid, int nt)
+{
+    constexpr int NP = 1 + O + (A - 1);
+    const int nw = nfin * A * NP;
+    for (int base = 0; base < nw; base += nt) {
+        const int w = base + tid;
+        const bool on = w < nw;
+        const int wc = on ? w : 0;
+        const int fe = wc / (A * NP), rem = wc - fe * (A * NP);
+        const int ag = rem / NP, p = rem - ag * NP;
+        const int c = list[fe];
+        const float *s = ev.state(c) + 5 * ag;
+        const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
+        const float *pt;
+        int sa, sd;
+        if (p == 0) {            // target
+            pt = ev.targ(c);
+            sa = 0;
+            sd = 1;
+        } else if (p <= O) {     // obstacle p - 1
+            pt = ev.obst(c) + 2 * (p - 1);
+            sa = 1 + p;
+            sd = 1 + O + p;
+        } else {                 // other agent kx, skipping self
+            const int kx = p - O - 1;
+            pt = ev.state(c) + 5 * (kx + (kx >= ag ? 1 : 0));
+            sa = 2 + 2 * O + kx;
+            sd = 2 + 2 * O + (A - 1) + kx;
+        }
+        const float px = pt[0], py = pt[1];
+        const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+        bool unused = true;
+        float d, ang;
+        if (__ballot(on && !cok) == 0ull) {
+            d = pair_dist<true>(ox, oy, px, py, unused);
+            ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+        } else {
+            d = pair_dist<false>(ox, oy, px, py, unused);
+            ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+        }
+        if (on) {
+            float *o = ev.row(c, ag);
+            o[sa] = ang;
+            o[sd] = d;
+        }
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void lds_row_write(float *dst, const float *row)
+{
+    if constexpr (D % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 4)
+            *reinterpret_cast<float4 *>(dst + k) = make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]);
+    } else if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 2)
+            *reinterpret_cast<float2 *>(dst + k) = make_float2(row[k], row[k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) dst[k] = row[k];
+    }
+}
+
+// Re-initialisation of the finished envs (environment.py:76-90, the sampler
+// call at :78) spread over the workgroup: one item per thread per pass - one
+// float of a fresh candidate (reference RNG) or of the formation template,
+// or one Philox block of two obstacles (native; the same draws as
+// native_fresh_env). Writes the LDS state and the global obstacles / target;
+// the agent rows go out with the final stores.
+template <int A, int O, class Envs, class List>
+__device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const float *form,
+                                             const List &list, int nfin, int tid, int nt)
+{
+    float *gob = kl->a.b.obstacles;
+    float *gtg = kl->a.b.target;
+    const float *fs = kl->a.b.fresh_states;
+    if (fs) {
+        const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
+        const bool keep = (kl->p.flags & MARLNAV_FRESH_STATES_FROM_MOVED) != 0;
+        constexpr int NI = 5 * A + 2 * O + 2;
+        for (int i = tid; i < nfin * NI; i += nt) {
+            const int fe = i / NI, kk = i - fe * NI;
+            const int c = list[fe];
+            const int64_t e = ev.env(c);
+            if (kk < 5 * A) {
+                if (!keep) ev.state(c)[kk] = fs[e * A * 5 + kk];
+            } else if (kk < 5 * A + 2 * O) {
+                const int j = kk - 5 * A;
+                const float v = fo[e * O * 2 + j];
+                ev.obst(c)[j] = v;
+                gob[e * O * 2 + j] = v;
+            } else {
+                const int j = kk - 5 * A - 2 * O;
+                const float v = ft[2 * e + j];
+                ev.targ(c)[j] = v;
+                gtg[2 * e + j] = v;
+            }
+        }
+        return;
+    }
+    constexpr int NB = (O + 1) / 2, NI = 5 * A + 2 + NB;
+    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
+    const int64_t eoff = kl->a.env_offset;
+    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
+    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
+    for (int i = tid; i < nfin * NI; i += nt) {
+        const int fe = i / NI, kk = i - fe * NI;
+        const int c = list[fe];
+        const int64_t e = ev.env(c);
+        if (kk < 5 * A) {
+            ev.state(c)[kk] = form[kk];
+        } else if (kk < 5 * A + 2) {
+            const int j = kk - 5 * A;
+            ev.targ(c)[j] = form[kk];
+            gtg[2 * e + j] = form[kk];
+        } else {
+            const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
+            const uint64_t gid = (uint64_t)(eoff + e);
+            uint32_t cc[4] = {(uint32_t)jb, (uint32_t)sidx, (uint32_t)gid,
+                              (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
+            philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
+            const int j = 2 * jb;
+            float *o = ev.obst(c) + 2 * j;
+            float *g = gob + e * O * 2 + 2 * j;
+            o[0] = g[0] = rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+            o[1] = g[1] = ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
+            if (j + 1 < O) {
+                o[2] = g[2] = rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+                o[3] = g[3] = ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
+            }
+        }
+    }
+}
+
+// Native (non-noisy) re-init and re-observation of the finished envs in ONE
+// pass over the workgroup: a fresh env's agent rows and target are the
+// formation template and its obstacles are Philox draws (the same as
+// native_fresh_env), so each observation item computes its own inputs
+// instead of waiting for a re-init pass and a barrier. Items per finished
+// env: A*(1+O+A-1) pairs (written into the packed rows), 5A+2 template
+// floats and ceil(O/2) Philox blocks (written to the LDS state and the
+// global obstacles/target).
+template <int A, int O, class Envs, class List>
+__device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, const float *form,
+                                                    const List &list, int nfin, float cap, int tid,
+                                                    int nt)
+{
+    constexpr int NP = 1 + O + (A - 1), NB = (O + 1) / 2;
+    constexpr int NPAIR = A * NP, NI = NPAIR + 5 * A + 2 + NB;
+    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
+    const int64_t eoff = kl->a.env_offset;
+    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
+    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
+    float *gob = kl->a.b.obstacles;
+    float *gtg = kl->a.b.target;
+    const int n = nfin * NI;
+    for (int base = 0; base < n; base += nt) {
+        const int i = base + tid;
+        const bool on = i < n;
+        const int ic = on ? i : 0;
+        const int fe = ic / NI, kk = ic - fe * NI;
+        const int c = list[fe];
+        const int64_t e = ev.env(c);
+        const uint64_t gid = (uint64_t)(eoff + e);
+        const bool pair = kk < NPAIR;
+        // Philox block: obstacle pair items (the block of their obstacle) and
+        // obstacle store items
+        int jb = -1;
+        int ag = 0, p = 0;
+        if (pair) {
+            ag = kk / NP;
+            p = kk - ag * NP;
+            if (p >= 1 && p <= O) jb = (p - 1) >> 1;
+        } else if (kk >= NPAIR + 5 * A + 2) {
+            jb = kk - (NPAIR + 5 * A + 2);
+        }
+        uint32_t cc[4] = {0u, 0u, 0u, 0u};
+        if (jb >= 0) {
+            cc[0] = (uint32_t)jb;
+            cc[1] = (uint32_t)sidx;
+            cc[2] = (uint32_t)gid;
+            cc[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
+            philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
+        }
+        if (pair) {
+            const float *s = form + 5 * ag;
+            const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
+            float px, py;
+            int sa, sd;
+            if (p == 0) {            // target
+                px = form[5 * A];
+                py = form[5 * A + 1];
+                sa = 0;
+                sd = 1;
+            } else if (p <= O) {     // obstacle p - 1: components of its Philox block
+                const bool hi = ((p - 1) & 1) != 0;
+                const uint32_t ux = hi ? cc[2] : cc[0], uy = hi ? cc[3] : cc[1];
+                px = rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx;
+                py = ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my;
+                sa = 1 + p;
+                sd = 1 + O + p;
+            } else {                 // other agent kx, skipping self
+                const int kx = p - O - 1;
+                const float *q = form + 5 * (kx + (kx >= ag ? 1 : 0));
+                px = q[0];
+                py = q[1];
+                sa = 2 + 2 * O + kx;
+                sd = 2 + 2 * O + (A - 1) + kx;
+            }
+            const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+            bool unused = true;
+            float d, ang;
+            if (__ballot(on && !cok) == 0ull) {
+                d = pair_dist<true>(ox, oy, px, py, unused);
+                ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+            } else {
+                d = pair_dist<false>(ox, oy, px, py, unused);
+                ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+            }
+            if (on) {
+                float *o = ev.row(c, ag);
+                o[sa] = ang;
+                o[sd] = d;
+            }
+        } else if (on) {
+            const int k2 = kk - NPAIR;
+            if (k2 < 5 * A) {
+                ev.state(c)[k2] = form[k2];
+            } else if (k2 < 5 * A + 2) {
+                const int j = k2 - 5 * A;
+                ev.targ(c)[j] = form[k2];
+                gtg[2 * e + j] = form[k2];
+            } else {
+                const int j = 2 * jb;
+                float *o = ev.obst(c) + 2 * j;
+                float *g = gob + e * O * 2 + 2 * j;
+                o[0] = g[0] = rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+                o[1] = g[1] = ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
+                if (j + 1 < O) {
+                    o[2] = g[2] = rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+                    o[3] = g[3] = ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
+                }
+            }
+        }
+    }
+}
+
+// Finished envs of a split-kernel workgroup: wave w listed cnt[w] env codes
+// (w * EPW + env) in slot[w * EPW ...]; entry fe of the concatenation.
+template <int EPW>
+struct SplitFinList {
+    int off1, off2, off3, n;  // prefix sums over the (up to 4) live waves
+    const int *slot;
+    __device__ static SplitFinList make(const int *cnt, const int *slot, int live)
+    {
+        static_assert(kWavesPerBlock == 4, "four waves per workgroup");
+        const int c0 = cnt[0];
+        const int c1 = live > 1 ? cnt[1] : 0;
+        const int c2 = live > 2 ? cnt[2] : 0;
+        const int c3 = live > 3 ? cnt[3] : 0;
+        return SplitFinList{c0, c0 + c1, c0 + c1 + c2, c0 + c1 + c2 + c3, slot};
+    }
+    __device__ int total() const { return n; }
+    __device__ int operator[](int fe) const
+    {
+        const int w = (fe >= off1) + (fe >= off2) + (fe >= off3);
+        const int base = w == 0 ? 0 : (w == 1 ? off1 : (w == 2 ? off2 : off3));
+        return slot[w * EPW + fe - base];
+    }
+};
+
+// Finished envs re-initialised and re-observed by the whole workgroup
+// (after one block barrier) instead of by their own wave: pays where an
+// env's re-observation is long (measured: A3/O8 and A16/O32 faster, A3/O3
+// slower). MARLNAV_SPLIT_SPREAD=0 turns it off (A/B builds).
+#ifndef MARLNAV_SPLIT_SPREAD
+#define MARLNAV_SPLIT_SPREAD 1
+#endif
+template <int A, int O>
+constexpr bool kSplitSpread = MARLNAV_SPLIT_SPREAD != 0 && A * (1 + O + (A - 1)) >= 32;
+
 template <int A, int O, int LPR>
 struct SplitPlan {
     static constexpr int EPW = 64 / LPR / A;  // envs per wave
@@ -1696,10 +2048,13 @@ struct SplitPlan {
     static constexpr int OB = (ACT + R * 2 + 3) & ~3;      // (EPW, O, 2)
     static constexpr int TG = (OB + EPW * O * 2 + 3) & ~3; // (EPW, 2)
     static constexpr int SN = (TG + EPW * 2 + 3) & ~3;     // (EPW,)
-    static constexpr int OBS = (SN + EPW + 3) & ~3;        // (R, D)
-    static constexpr int BOND = (OBS + R * D + 3) & ~3;    // (R, A-1)
+    static constexpr int DP = split_row_stride(D, LPR, R < 32 / LPR ? R : 32 / LPR);
+    static constexpr int OBS = (SN + EPW + 3) & ~3;        // (R, DP)
+    static constexpr int BOND = (OBS + R * DP + 3) & ~3;   // (R, A-1)
     static constexpr int RED = (BOND + R * (A - 1) + 3) & ~3;  // (R, 4)
     static constexpr int FLOATS = RED + 4 * R;
+    // after the waves' regions: finished-env counts and slots of the workgroup
+    static constexpr int BLK = (kWavesPerBlock * (1 + EPW) + 3) & ~3;
     static_assert(EPW >= 1, "an env's rows must fit one wave");
 };
 
@@ -1758,6 +2113,27 @@ struct SplitTerms {
     float ta, td;
 };
 
+// Occupancy the register allocator may assume (waves per SIMD): the grids
+// below run at most 3-4 waves per SIMD, so the default target of 8 only
+// costs instruction-level parallelism (timing builds set these).
+#ifdef MARLNAV_SPLIT_WPE
+#define MARLNAV_SPLIT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(MARLNAV_SPLIT_WPE)))
+#else
+#define MARLNAV_SPLIT_WPE_ATTR
+#endif
+#ifdef MARLNAV_BLOCK_WPE
+#define MARLNAV_BLOCK_WPE_ATTR __attribute__((amdgpu_waves_per_eu(MARLNAV_BLOCK_WPE)))
+#else
+#define MARLNAV_BLOCK_WPE_ATTR
+#endif
+
+// unroll factor of split_pairs' obstacle / other-agent loops (timing builds)
+#ifndef MARLNAV_SPLIT_UNROLL
+#define MARLNAV_SPLIT_UNROLL 64
+#endif
+#define MARLNAV_PRAGMA(x) _Pragma(#x)
+#define MARLNAV_UNROLL(n) MARLNAV_PRAGMA(unroll n)
+
 template <int A, int O, int LPR, bool TERMS, bool FAST>
 __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
                                                   const float *__restrict__ obe,
@@ -1780,7 +2156,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
             orow[1] = d;
         }
     }
-#pragma unroll
+    MARLNAV_UNROLL(MARLNAV_SPLIT_UNROLL)
     for (int i = 0; i < SP::NOB; ++i) {
         const int j = q + LPR * i;
         if (O % LPR == 0 || j < O) {
@@ -1792,7 +2168,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
                 t.fl |= (d < pr.ob_risk_dist ? 1u : 0u) | (d < pr.ob_coll_dist ? 2u : 0u);
         }
     }
-#pragma unroll
+    MARLNAV_UNROLL(MARLNAV_SPLIT_UNROLL)
     for (int i = 0; i < SP::NAG; ++i) {
         const int kx = q + LPR * i;  // index among the others
         if ((A - 1) % LPR == 0 || kx < A - 1) {
@@ -1818,7 +2194,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
 }
 
 template <int A, int O, int LPR, bool OBS_ONLY, bool NOISY>
-__global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
+__global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR split_kernel(KArgs k)
 {
     using SP = SplitPlan<A, O, LPR>;
     constexpr int EPW = SP::EPW, R = SP::R, D = SP::D;
@@ -1913,7 +2289,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
     const float *sts = st + 5 * A * el;
     const float *obe = wl + SP::OB + 2 * O * el;
     const float *tge = wl + SP::TG + 2 * el;
-    float *orow = wl + SP::OBS + rowc * D;
+    float *orow = wl + SP::OBS + rowc * SP::DP;
     float *brow = wl + SP::BOND + rowc * (A - 1);
     {
         // wave-uniform choice of the pair math (coord_ok, as in tile_kernel);
@@ -2009,7 +2385,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
             b.terminated[e] = (uint8_t)terminated;
             b.truncated[e] = (uint8_t)truncated;
             fin = truncated || terminated;                     // :102-104
-            if (fin) {
+            if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
                 KArgsK *kl = kargs_late();
                 MarlnavParams p;  // the fields the re-init reads
                 p.obs_range_x = kl->p.obs_range_x;
@@ -2027,7 +2403,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
                 const float *fs = kl->a.b.fresh_states;
                 float *gob = kl->a.b.obstacles;
                 float *gtg = kl->a.b.target;
-                if (fs) {
+                if (!NOISY && fs) {
                     const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
                     if (!(p.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
                         for (int i = 0; i < 5 * A; ++i) s5[i] = fs[e * A * 5 + i];
@@ -2042,8 +2418,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
                 for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
                 gtg[2 * e] = tgl[0];
                 gtg[2 * e + 1] = tgl[1];
-                step_num = 0.0f;
             }
+            if (fin) step_num = 0.0f;
             b.step_num[e] = step_num;
             tr_l = truncated;
             co_l = any_col;
@@ -2055,8 +2431,46 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
         c_tar = __popcll(__ballot(ta_l));
         STAMP(4);
 
-        // ---- observations of re-initialised envs (:105)
-        if (finmask) {
+        if constexpr (kSplitSpread<A, O>) {
+            // ---- the workgroup's finished envs, re-initialised (:104) and
+            // re-observed (:105) by all its threads: a finished env costs its
+            // wave ~1/4 of a full observation pass instead of a second pass
+            // on its own lanes (the straggler that set the kernel's end)
+            int *bcnt = reinterpret_cast<int *>(lds + kWavesPerBlock * SP::FLOATS);
+            int *bslot = bcnt + kWavesPerBlock;
+            if (fin)
+                bslot[wib * EPW + (int)__builtin_amdgcn_mbcnt_hi(
+                                      (unsigned)(finmask >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] =
+                    wib * EPW + (int)lane;
+            if (lane == 0) bcnt[wib] = (int)__popcll(finmask);
+            __syncthreads();
+            const int64_t blk0 = (int64_t)blockIdx.x * kWavesPerBlock;
+            const int live = (int)(K->a.ntiles - blk0 < kWavesPerBlock ? K->a.ntiles - blk0
+                                                                      : kWavesPerBlock);
+            const SplitFinList<EPW> list = SplitFinList<EPW>::make(bcnt, bslot, live);
+            if (const int nfin = list.total()) {
+                KArgsK *kl = kargs_late();
+                const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
+                    lds, blk0 * EPW};
+                // waves past the last tile have exited: items go to the live ones
+                const int tid = (int)threadIdx.x, nt = 64 * live;
+                // fused native re-init + re-observation recomputes a Philox
+                // block per obstacle pair: only for few obstacles
+                if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
+                    reinit_reobs_native<A, O>(kl, ev, kl->a.b.formation, list, nfin,
+                                              pr.cap_distance, tid, nt);
+                } else {
+                    if (!NOISY) {
+                        reinit_block<A, O>(kl, ev, kl->a.b.formation, list, nfin, tid, nt);
+                        __syncthreads();
+                    }
+                    reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
+                }
+                __syncthreads();
+            }
+        } else if (finmask) {
+            // ---- observations of re-initialised envs (:105), on the wave
             wave_sync();
             const bool redo = row_on && ((finmask >> el) & 1u);
             const float *s = st + 5 * rowc;
@@ -2095,7 +2509,22 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
             mean = kl->a.b.norm_mean;
             scale = kl->a.b.norm_scale;
         }
-        if (VAL % 16 == 0 && ne == EPW) {
+        if constexpr (SP::DP != D) {  // padded rows (D % 4 == 0): 16-byte pieces
+            static_assert(D % 4 == 0 && SP::DP % 4 == 0, "padded rows keep 16-byte alignment");
+            constexpr int D4 = D / 4;
+            if (VAL % 16 == 0) {
+                for (int i = (int)lane; i < n / 4; i += 64) {
+                    const int rr = i / D4, c4 = i - rr * D4;
+                    reinterpret_cast<float4 *>(gobs)[i] =
+                        *reinterpret_cast<const float4 *>(src + rr * SP::DP + 4 * c4);
+                }
+            } else {
+                for (int i = (int)lane; i < n; i += 64) {
+                    const int rr = i / D;
+                    gobs[i] = src[rr * SP::DP + (i - rr * D)];
+                }
+            }
+        } else if (VAL % 16 == 0 && ne == EPW) {
             for (int i = (int)lane; i < n / 4; i += 64)
                 reinterpret_cast<float4 *>(gobs)[i] = reinterpret_cast<const float4 *>(src)[i];
         } else if (VAL % 8 == 0 && n % 2 == 0) {
@@ -2106,8 +2535,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
         }
         if (gnorm)
             for (int i = (int)lane; i < n; i += 64) {
-                const int kk = i % D;
-                gnorm[i] = (src[i] - mean[kk]) / scale[kk];
+                const int rr = i / D, kk = i - rr * D;
+                gnorm[i] = (src[rr * SP::DP + kk] - mean[kk]) / scale[kk];
             }
     }
     if (!OBS_ONLY) {
@@ -2205,264 +2634,6 @@ __device__ __forceinline__ void block_store(float *__restrict__ dst, const float
     for (int i = (n4 << 2) + tid; i < n; i += nt) dst[i] = src[i];
 }
 
-// Re-observation of the finished envs (environment.py:105) spread over the
-// block: one (row, pair) item per thread per pass, results written straight
-// into the block's packed rows. Per wave and pass, the short sqrt/division
-// sequences run when every coordinate of the pass passes coord_ok, IEEE
-// otherwise.
-template <int A, int O>
-__device__ __forceinline__ void reobs_block(const float *st, const float *ob, const float *tg,
-                                            const int *list, int nfin, float *obs_rows,
-                                            float cap, int tid, int nt)
-{
-    constexpr int NP = 1 + O + (A - 1), D = 2 + 2 * O + 2 * (A - 1);
-    const int nw = nfin * A * NP;
-    for (int base = 0; base < nw; base += nt) {
-        const int w = base + tid;
-        const bool on = w < nw;
-        const int wc = on ? w : 0;
-        const int fe = wc / (A * NP), rem = wc - fe * (A * NP);
-        const int ag = rem / NP, p = rem - ag * NP;
-        const int env = list[fe];
-        const float *s = st + 5 * (env * A + ag);
-        const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
-        const float *pt;
-        int sa, sd;
-        if (p == 0) {            // target
-            pt = tg + 2 * env;
-            sa = 0;
-            sd = 1;
-        } else if (p <= O) {     // obstacle p - 1
-            pt = ob + 2 * (env * O + p - 1);
-            sa = 1 + p;
-            sd = 1 + O + p;
-        } else {                 // other agent kx, skipping self
-            const int kx = p - O - 1;
-            pt = st + 5 * (env * A + kx + (kx >= ag ? 1 : 0));
-            sa = 2 + 2 * O + kx;
-            sd = 2 + 2 * O + (A - 1) + kx;
-        }
-        const float px = pt[0], py = pt[1];
-        const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
-        bool unused = true;
-        float d, ang;
-        if (__ballot(on && !cok) == 0ull) {
-            d = pair_dist<true>(ox, oy, px, py, unused);
-            ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
-        } else {
-            d = pair_dist<false>(ox, oy, px, py, unused);
-            ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
-        }
-        if (on) {
-            float *o = obs_rows + (env * A + ag) * D;
-            o[sa] = ang;
-            o[sd] = d;
-        }
-    }
-}
-
-template <int D>
-__device__ __forceinline__ void lds_row_write(float *dst, const float *row)
-{
-    if constexpr (D % 4 == 0) {
-#pragma unroll
-        for (int k = 0; k < D; k += 4)
-            *reinterpret_cast<float4 *>(dst + k) = make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]);
-    } else if constexpr (D % 2 == 0) {
-#pragma unroll
-        for (int k = 0; k < D; k += 2)
-            *reinterpret_cast<float2 *>(dst + k) = make_float2(row[k], row[k + 1]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < D; ++k) dst[k] = row[k];
-    }
-}
-
-// Re-initialisation of the finished envs (environment.py:76-90, the sampler
-// call at :78) spread over the block: one item per thread per pass - one
-// float of a fresh candidate (reference RNG) or of the formation template,
-// or one Philox block of two obstacles (native; the same draws as
-// native_fresh_env). Writes the block's LDS state and the global obstacles /
-// target; the agent rows go out with the block's final stores.
-template <int A, int O>
-__device__ __forceinline__ void reinit_block(KArgsK *kl, float *st, float *ob, float *tg,
-                                             const float *form, const int *list, int nfin,
-                                             int64_t e0, int tid, int nt)
-{
-    float *gob = kl->a.b.obstacles;
-    float *gtg = kl->a.b.target;
-    const float *fs = kl->a.b.fresh_states;
-    if (fs) {
-        const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
-        const bool keep = (kl->p.flags & MARLNAV_FRESH_STATES_FROM_MOVED) != 0;
-        constexpr int NI = 5 * A + 2 * O + 2;
-        for (int i = tid; i < nfin * NI; i += nt) {
-            const int fe = i / NI, kk = i - fe * NI;
-            const int env = list[fe];
-            const int64_t e = e0 + env;
-            if (kk < 5 * A) {
-                if (!keep) st[5 * A * env + kk] = fs[e * A * 5 + kk];
-            } else if (kk < 5 * A + 2 * O) {
-                const int j = kk - 5 * A;
-                const float v = fo[e * O * 2 + j];
-                ob[2 * O * env + j] = v;
-                gob[e * O * 2 + j] = v;
-            } else {
-                const int j = kk - 5 * A - 2 * O;
-                const float v = ft[2 * e + j];
-                tg[2 * env + j] = v;
-                gtg[2 * e + j] = v;
-            }
-        }
-        return;
-    }
-    constexpr int NB = (O + 1) / 2, NI = 5 * A + 2 + NB;
-    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
-    const int64_t eoff = kl->a.env_offset;
-    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
-    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
-    for (int i = tid; i < nfin * NI; i += nt) {
-        const int fe = i / NI, kk = i - fe * NI;
-        const int env = list[fe];
-        const int64_t e = e0 + env;
-        if (kk < 5 * A) {
-            st[5 * A * env + kk] = form[kk];
-        } else if (kk < 5 * A + 2) {
-            const int j = kk - 5 * A;
-            tg[2 * env + j] = form[kk];
-            gtg[2 * e + j] = form[kk];
-        } else {
-            const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
-            const uint64_t gid = (uint64_t)(eoff + e);
-            uint32_t c[4] = {(uint32_t)jb, (uint32_t)sidx, (uint32_t)gid,
-                             (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
-            philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-            const int j = 2 * jb;
-            float *o = ob + 2 * O * env + 2 * j;
-            float *g = gob + e * O * 2 + 2 * j;
-            o[0] = g[0] = rx * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-            o[1] = g[1] = ry * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
-            if (j + 1 < O) {
-                o[2] = g[2] = rx * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-                o[3] = g[3] = ry * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
-            }
-        }
-    }
-}
-
-// Native (non-noisy) re-init and re-observation of the finished envs in ONE
-// pass over the block: a fresh env's agent rows and target are the formation
-// template and its obstacles are Philox draws (the same as native_fresh_env),
-// so each observation item computes its own inputs instead of waiting for a
-// re-init pass and a barrier. Items per finished env: A*(1+O+A-1) pairs
-// (written into the packed rows), 5A+2 template floats and ceil(O/2) Philox
-// blocks (written to the LDS state and the global obstacles/target).
-template <int A, int O>
-__device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, float *st, float *ob, float *tg,
-                                                    const float *form, const int *list, int nfin,
-                                                    float *obs_rows, float cap, int64_t e0,
-                                                    int tid, int nt)
-{
-    constexpr int NP = 1 + O + (A - 1), D = 2 + 2 * O + 2 * (A - 1), NB = (O + 1) / 2;
-    constexpr int NPAIR = A * NP, NI = NPAIR + 5 * A + 2 + NB;
-    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
-    const int64_t eoff = kl->a.env_offset;
-    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
-    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
-    float *gob = kl->a.b.obstacles;
-    float *gtg = kl->a.b.target;
-    const int n = nfin * NI;
-    for (int base = 0; base < n; base += nt) {
-        const int i = base + tid;
-        const bool on = i < n;
-        const int ic = on ? i : 0;
-        const int fe = ic / NI, kk = ic - fe * NI;
-        const int env = list[fe];
-        const int64_t e = e0 + env;
-        const uint64_t gid = (uint64_t)(eoff + e);
-        const bool pair = kk < NPAIR;
-        // Philox block: obstacle pair items (the block of their obstacle) and
-        // obstacle store items
-        int jb = -1;
-        int ag = 0, p = 0;
-        if (pair) {
-            ag = kk / NP;
-            p = kk - ag * NP;
-            if (p >= 1 && p <= O) jb = (p - 1) >> 1;
-        } else if (kk >= NPAIR + 5 * A + 2) {
-            jb = kk - (NPAIR + 5 * A + 2);
-        }
-        uint32_t c[4] = {0u, 0u, 0u, 0u};
-        if (jb >= 0) {
-            c[0] = (uint32_t)jb;
-            c[1] = (uint32_t)sidx;
-            c[2] = (uint32_t)gid;
-            c[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
-            philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-        }
-        if (pair) {
-            const float *s = form + 5 * ag;
-            const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
-            float px, py;
-            int sa, sd;
-            if (p == 0) {            // target
-                px = form[5 * A];
-                py = form[5 * A + 1];
-                sa = 0;
-                sd = 1;
-            } else if (p <= O) {     // obstacle p - 1: components of its Philox block
-                const bool hi = ((p - 1) & 1) != 0;
-                const uint32_t ux = hi ? c[2] : c[0], uy = hi ? c[3] : c[1];
-                px = rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx;
-                py = ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my;
-                sa = 1 + p;
-                sd = 1 + O + p;
-            } else {                 // other agent kx, skipping self
-                const int kx = p - O - 1;
-                const float *q = form + 5 * (kx + (kx >= ag ? 1 : 0));
-                px = q[0];
-                py = q[1];
-                sa = 2 + 2 * O + kx;
-                sd = 2 + 2 * O + (A - 1) + kx;
-            }
-            const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
-            bool unused = true;
-            float d, ang;
-            if (__ballot(on && !cok) == 0ull) {
-                d = pair_dist<true>(ox, oy, px, py, unused);
-                ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
-            } else {
-                d = pair_dist<false>(ox, oy, px, py, unused);
-                ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
-            }
-            if (on) {
-                float *o = obs_rows + (env * A + ag) * D;
-                o[sa] = ang;
-                o[sd] = d;
-            }
-        } else if (on) {
-            const int k2 = kk - NPAIR;
-            if (k2 < 5 * A) {
-                st[5 * A * env + k2] = form[k2];
-            } else if (k2 < 5 * A + 2) {
-                const int j = k2 - 5 * A;
-                tg[2 * env + j] = form[k2];
-                gtg[2 * e + j] = form[k2];
-            } else {
-                const int j = 2 * jb;
-                float *o = ob + 2 * O * env + 2 * j;
-                float *g = gob + e * O * 2 + 2 * j;
-                o[0] = g[0] = rx * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-                o[1] = g[1] = ry * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
-                if (j + 1 < O) {
-                    o[2] = g[2] = rx * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-                    o[3] = g[3] = ry * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
-                }
-            }
-        }
-    }
-}
-
 #ifndef MARLNAV_BLK_EARLY  // 1: stream rows/states out before the per-env phase
 #define MARLNAV_BLK_EARLY 0
 #endif
@@ -2477,7 +2648,7 @@ constexpr bool kBlkSpread = MARLNAV_BLK_SPREAD != 0;
 // out while wave 0 runs the per-env phase | re-init, re-observe and re-store
 // the finished envs only (none in most blocks).
 template <int A, int O, bool OBS_ONLY, bool NOISY>
-__global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
+__global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KArgs k)
 {
     using BP = BlockPlan<A, O>;
     constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
@@ -2737,17 +2908,16 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
             // ---- masked re-init (:104) and observations of the re-initialised
             // envs (:105), then their rows and states go out again
             KArgsK *kl = kargs_late();
+            const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
             if (!NOISY && kBlkSpread && !kl->a.b.fresh_states) {
-                reinit_reobs_native<A, O>(kl, st, lds + BP::OB, lds + BP::TG, lds + BP::FORM,
-                                          list, nfin, obs_rows, pr.cap_distance, e0, tid, NT);
+                reinit_reobs_native<A, O>(kl, ev, lds + BP::FORM, list, nfin, pr.cap_distance,
+                                          tid, NT);
             } else {
                 if (!NOISY && kBlkSpread) {
-                    reinit_block<A, O>(kl, st, lds + BP::OB, lds + BP::TG, lds + BP::FORM, list,
-                                       nfin, e0, tid, NT);
+                    reinit_block<A, O>(kl, ev, lds + BP::FORM, list, nfin, tid, NT);
                     __syncthreads();
                 }
-                reobs_block<A, O>(st, lds + BP::OB, lds + BP::TG, list, nfin, obs_rows,
-                                  pr.cap_distance, tid, NT);
+                reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, NT);
             }
             __syncthreads();
             constexpr int NI = A * D + 5 * A;
@@ -2976,9 +3146,13 @@ struct SplitVariant {
 #define MARLNAV_SPLIT_VARIANT(A, O, LPR, ALWAYS)                                          \
     {A, O, SplitPlan<A, O, LPR>::EPW, split_kernel<A, O, LPR, false, false>,             \
      split_kernel<A, O, LPR, true, false>, split_kernel<A, O, LPR, false, true>,         \
-     (size_t)SplitPlan<A, O, LPR>::FLOATS * 4 * kWavesPerBlock, ALWAYS}
+     (size_t)(SplitPlan<A, O, LPR>::FLOATS * kWavesPerBlock + SplitPlan<A, O, LPR>::BLK) * 4, \
+     ALWAYS}
 const SplitVariant kSplitVariants[] = {
-    MARLNAV_SPLIT_VARIANT(16, 32, 4, true),
+#ifndef MARLNAV_C4_LPR  // lanes per agent row at A16/O32 (timing builds)
+#define MARLNAV_C4_LPR 4
+#endif
+    MARLNAV_SPLIT_VARIANT(16, 32, MARLNAV_C4_LPR, true),
     MARLNAV_SPLIT_VARIANT(3, 8, 4, false),
     MARLNAV_SPLIT_VARIANT(3, 3, 4, false),
 #ifdef MARLNAV_SPLIT33_LPR2

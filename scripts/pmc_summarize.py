@@ -6,11 +6,13 @@ STEP_KERNELS = ("wave_kernel", "tile_kernel", "split_kernel", "block_kernel")
 
 
 def is_step(name):
-    """A step launch (not the observe-only instantiation: OBS_ONLY is template arg 3)."""
+    """A step launch, not the observe-only instantiation (the OBS_ONLY
+    template argument: 4th of split_kernel, 3rd of the others)."""
     if not any(k in name for k in STEP_KERNELS):
         return False
     args = name[name.index("<") + 1:name.index(">")].split(",")
-    return len(args) >= 3 and args[2].strip() == "false"
+    i = 3 if "split_kernel" in name else 2
+    return len(args) > i and args[i].strip() == "false"
 
 dur = []
 for f in sorted(glob.glob(os.path.join(out, "p*", "run_counter_collection.csv"))):
