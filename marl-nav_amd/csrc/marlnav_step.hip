@@ -172,8 +172,10 @@ __device__ __forceinline__ float sqrt_fast(float x, bool &ok)
     float s = __builtin_amdgcn_sqrtf(x);
     const float s_dn = __int_as_float(__float_as_int(s) - 1);
     const float s_up = __int_as_float(__float_as_int(s) + 1);
-    const float r_dn = __builtin_fmaf(-s_dn, s, x);
-    const float r_up = __builtin_fmaf(-s_up, s, x);
+    // x - s_dn*s with the sign on the float operand (a free source modifier;
+    // negating the integer-built neighbour costs a v_xor per pair)
+    const float r_dn = __builtin_fmaf(s_dn, -s, x);
+    const float r_up = __builtin_fmaf(s_up, -s, x);
     s = r_dn <= 0.0f ? s_dn : s;
     return r_up > 0.0f ? s_up : s;
 }
@@ -272,7 +274,10 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
                                             bool &ok)
 {
     const float dx = px - ox, dy = py - oy;
-    const float den = dist > 1e-12f ? dist : 1e-12f;
+    // F.normalize's clamp_min(1e-12). FAST (finite, non-negative dist): one
+    // v_med3 instead of a canonicalize + v_max
+    const float den = FAST ? __builtin_amdgcn_fmed3f(dist, 1e-12f, __builtin_inff())
+                           : (dist > 1e-12f ? dist : 1e-12f);
 #if MARLNAV_ABLATE & 4
     const float nx = __fdividef(dx, den), ny = __fdividef(dy, den);
 #else
@@ -285,7 +290,9 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
     }
 #endif
     float dot = dirx * nx + diry * ny;
-    dot = clamp_t(dot, -1.0f, 1.0f);
+    // FAST: dot is finite, so the clamp is one v_med3 (no compare/select
+    // pairs and their VCC hazard nops); -0 passes through either way
+    dot = FAST ? __builtin_amdgcn_fmed3f(dot, -1.0f, 1.0f) : clamp_t(dot, -1.0f, 1.0f);
     const float orth_x = nx - dot * dirx;
 #if MARLNAV_ABLATE & 1
     const float ang = (orth_x > 0.0f ? -1.0f : 1.0f) * dot;
