@@ -2208,6 +2208,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
     (void)k;  // read through kargs_late()
     extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS
+    int stamp_nfin = 0;
+#endif
+#if MARLNAV_STAMPS
     unsigned long long t_entry;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
 #endif
@@ -2456,6 +2459,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
             const int live = (int)(K->a.ntiles - blk0 < kWavesPerBlock ? K->a.ntiles - blk0
                                                                       : kWavesPerBlock);
             const SplitFinList<EPW> list = SplitFinList<EPW>::make(bcnt, bslot, live);
+#if MARLNAV_STAMPS
+            stamp_nfin = list.total();
+#endif
             if (const int nfin = list.total()) {
                 KArgsK *kl = kargs_late();
                 const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
@@ -2576,6 +2582,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
         g_stamps[(size_t)gw * 24 + 16] = t_entry;
         g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
         g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 19] = (unsigned)stamp_nfin;
     }
 #endif
 }

@@ -93,6 +93,13 @@ def main():
             print(cfg, f"waves on {int(c)}-wave SIMDs: n={int(m.sum())} end p50/p90/max us",
                   [round(float(np.percentile(fin_all[m], q)), 2) for q in (50, 90, 100)],
                   "chain p50", round(float(np.median(rt[m, 7] - entry[m])), 2))
+        # the slowest 1% of waves: where their time went
+        slow = fin_all >= np.percentile(fin_all, 99)
+        print(cfg, "slowest 1% waves:", {"n": int(slow.sum()),
+              "entry_us": round(float(np.median(entry[slow] - t0)), 2),
+              "phase_median_us": {n: round(float(np.median(ph[slow, i])), 2)
+                                  for i, n in enumerate(names)},
+              "with_finished_envs": int((raw[slow, 19] > 0).sum())})
         # waves that re-observed finished envs vs the rest: do they set the end?
         reo = raw[:, 19] > 0  # tiles with a finished env (re-init + re-observe)
         fin_t = rt[:, 7] - t0
