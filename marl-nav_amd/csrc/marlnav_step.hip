@@ -102,6 +102,52 @@ __device__ __forceinline__ float clamp_t(float x, float lo, float hi)
     return x > hi ? hi : x;
 }
 
+// Observation rows and states of the env-block and pair-split kernels leave
+// through streaming stores (`nt`): nothing in the launch reads them back, and
+// dirty lines kept in the XCD's L2 only lengthen the end-of-launch
+// write-back. Measured: 65536x3x3 10.3 -> 9.4 us, 65536x3x8 13.0 -> 11.5 us,
+// 2^21 envs 150 -> 144 us, 4096x16x32 18.0 -> 17.3 us. Per-env scalars (one
+// env per wave in the split kernel: 1-4 byte stores) measured slower with nt
+// and stay plain, as do the tile/wave kernels' stores; MARLNAV_NT_STORES /
+// MARLNAV_NT_OTHER switch the two groups.
+#ifndef MARLNAV_NT_STORES
+#define MARLNAV_NT_STORES 1
+#endif
+#ifndef MARLNAV_NT_OTHER
+#define MARLNAV_NT_OTHER 0
+#endif
+constexpr bool kNtRows = MARLNAV_NT_STORES != 0;
+constexpr bool kNtOther = MARLNAV_NT_OTHER != 0;
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+
+template <bool NT = kNtOther, class T>
+__device__ __forceinline__ void out_st(T *p, T v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <bool NT = kNtOther>
+__device__ __forceinline__ void out_st4(float *p, float4 v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v4f_t{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f_t *>(p));
+    else
+        *reinterpret_cast<float4 *>(p) = v;
+}
+
+template <bool NT = kNtOther>
+__device__ __forceinline__ void out_st2(float *p, float2 v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v2f_t{v.x, v.y}, reinterpret_cast<v2f_t *>(p));
+    else
+        *reinterpret_cast<float2 *>(p) = v;
+}
+
 // Fast-path switches for the pair math in FAST mode: 1 = the shortened
 // sequence (bit-exact inside its guard, scripts/probes/fastmath_probe.hip),
 // 0 = the IEEE operation. The tile kernels enter FAST mode only for a wave
@@ -567,13 +613,11 @@ __device__ __forceinline__ void wave_store(float *__restrict__ dst, const float 
     int head = 0;
     if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
         const int n4 = n >> 2;
-        for (int i = lane; i < n4; i += 64) {
-            const float4 v = *reinterpret_cast<const float4 *>(src + 4 * i);
-            *reinterpret_cast<float4 *>(dst + 4 * i) = v;
-        }
+        for (int i = lane; i < n4; i += 64)
+            out_st4(dst + 4 * i, *reinterpret_cast<const float4 *>(src + 4 * i));
         head = n4 << 2;
     }
-    for (int i = head + lane; i < n; i += 64) dst[i] = src[i];
+    for (int i = head + lane; i < n; i += 64) out_st(dst + i, src[i]);
     if (nrm_dst) {
         for (int i = lane; i < n; i += 64) {
             const int k = i % D;
@@ -832,14 +876,13 @@ __device__ __forceinline__ void store_row(float *__restrict__ dst, const float *
     if constexpr (D % 4 == 0) {
 #pragma unroll
         for (int k = 0; k < D; k += 4)
-            *reinterpret_cast<float4 *>(dst + k) = make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]);
+            out_st4(dst + k, make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]));
     } else if constexpr (D % 2 == 0) {
 #pragma unroll
-        for (int k = 0; k < D; k += 2)
-            *reinterpret_cast<float2 *>(dst + k) = make_float2(row[k], row[k + 1]);
+        for (int k = 0; k < D; k += 2) out_st2(dst + k, make_float2(row[k], row[k + 1]));
     } else {
 #pragma unroll
-        for (int k = 0; k < D; ++k) dst[k] = row[k];
+        for (int k = 0; k < D; ++k) out_st(dst + k, row[k]);
     }
 }
 
@@ -1031,15 +1074,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                 }
                 const float *rr = all_in ? rhit : rmiss;
                 const float rsum = torch_row_sum(rr + lane * A, A, [](float r) { return r; });
-                b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
+                out_st(&b.reward[e], rsum / (float)A);                     // torch.mean (:233)
 
                 float step_num = step_num_in + 1.0f;               // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = term_in != 0;
                 const bool terminated = any_col || term_old;       // :213-214
-                b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
-                b.terminated[e] = (uint8_t)terminated;
-                b.truncated[e] = (uint8_t)truncated;
+                out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
+                out_st(&b.terminated[e], (uint8_t)terminated);
+                out_st(&b.truncated[e], (uint8_t)truncated);
                 fin = truncated || terminated;                     // :102-104
                 if (fin) {
                     float *sts = st + 5 * A * lane;
@@ -1061,7 +1104,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                     b.target[2 * e + 1] = tge[1];
                     step_num = 0.0f;
                 }
-                b.step_num[e] = step_num;
+                out_st(&b.step_num[e], step_num);
                 envbits[lane] = fin ? 1u : 0u;
                 tr_l = truncated;
                 co_l = any_col;
@@ -1523,15 +1566,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
                 bool okq = MARLNAV_FM_TERMS != 0;                                    // torch.mean (:233)
                 float rmean = MARLNAV_FM_TERMS ? div_c(rsum, make_divc((float)A, okq), okq) : 0.0f;
                 if (__builtin_expect(!okq, 0)) rmean = rsum / (float)A;
-                b.reward[e] = rmean;
+                out_st(&b.reward[e], rmean);
 
                 float step_num = cur[TP::SN + lane] + 1.0f;        // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = reinterpret_cast<const uint8_t *>(cur + TP::TM)[lane] != 0;
                 const bool terminated = any_col || term_old;       // :213-214
-                b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
-                b.terminated[e] = (uint8_t)terminated;
-                b.truncated[e] = (uint8_t)truncated;
+                out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
+                out_st(&b.terminated[e], (uint8_t)terminated);
+                out_st(&b.truncated[e], (uint8_t)truncated);
                 fin = truncated || terminated;                     // :102-104
                 if (fin) {
                     KArgsK *kl = kargs_late();
@@ -1568,7 +1611,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
                     gtg[2 * e + 1] = tgl[1];
                     step_num = 0.0f;
                 }
-                b.step_num[e] = step_num;
+                out_st(&b.step_num[e], step_num);
                 tr_l = truncated;
                 co_l = any_col;
                 ta_l = all_in;
@@ -1649,10 +1692,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
                 for (int kk = 0; kk * 64 < N16; ++kk) {
                     const int i = kk * 64 + (int)lane;
                     if ((kk + 1) * 64 <= N16 || i < N16)
-                        reinterpret_cast<float4 *>(gst)[i] = reinterpret_cast<const float4 *>(st)[i];
+                        out_st4(gst + 4 * i, reinterpret_cast<const float4 *>(st)[i]);
                 }
             } else {
-                for (int i = (int)lane; i < nr * 5; i += 64) gst[i] = st[i];
+                for (int i = (int)lane; i < nr * 5; i += 64) out_st(gst + i, st[i]);
             }
         }
     }
@@ -2386,14 +2429,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
             bool okq = MARLNAV_FM_TERMS != 0;                                    // torch.mean (:233)
             float rmean = MARLNAV_FM_TERMS ? div_c(rsum, make_divc((float)A, okq), okq) : 0.0f;
             if (__builtin_expect(!okq, 0)) rmean = rsum / (float)A;
-            b.reward[e] = rmean;
+            out_st(&b.reward[e], rmean);
             float step_num = sn_in + 1.0f;                     // :96
             const bool truncated = step_num > pr.trunc_after;  // :97
             const bool term_old = term_in != 0u;
             const bool terminated = any_col || term_old;       // :213-214
-            b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
-            b.terminated[e] = (uint8_t)terminated;
-            b.truncated[e] = (uint8_t)truncated;
+            out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
+            out_st(&b.terminated[e], (uint8_t)terminated);
+            out_st(&b.truncated[e], (uint8_t)truncated);
             fin = truncated || terminated;                     // :102-104
             if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
                 KArgsK *kl = kargs_late();
@@ -2430,7 +2473,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
                 gtg[2 * e + 1] = tgl[1];
             }
             if (fin) step_num = 0.0f;
-            b.step_num[e] = step_num;
+            out_st(&b.step_num[e], step_num);
             tr_l = truncated;
             co_l = any_col;
             ta_l = all_in;
@@ -2528,23 +2571,22 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
             if (VAL % 16 == 0) {
                 for (int i = (int)lane; i < n / 4; i += 64) {
                     const int rr = i / D4, c4 = i - rr * D4;
-                    reinterpret_cast<float4 *>(gobs)[i] =
-                        *reinterpret_cast<const float4 *>(src + rr * SP::DP + 4 * c4);
+                    out_st4<kNtRows>(gobs + 4 * i, *reinterpret_cast<const float4 *>(src + rr * SP::DP + 4 * c4));
                 }
             } else {
                 for (int i = (int)lane; i < n; i += 64) {
                     const int rr = i / D;
-                    gobs[i] = src[rr * SP::DP + (i - rr * D)];
+                    out_st<kNtRows>(gobs + i, src[rr * SP::DP + (i - rr * D)]);
                 }
             }
         } else if (VAL % 16 == 0 && ne == EPW) {
             for (int i = (int)lane; i < n / 4; i += 64)
-                reinterpret_cast<float4 *>(gobs)[i] = reinterpret_cast<const float4 *>(src)[i];
+                out_st4<kNtRows>(gobs + 4 * i, reinterpret_cast<const float4 *>(src)[i]);
         } else if (VAL % 8 == 0 && n % 2 == 0) {
             for (int i = (int)lane; i < n / 2; i += 64)
-                reinterpret_cast<float2 *>(gobs)[i] = reinterpret_cast<const float2 *>(src)[i];
+                out_st2<kNtRows>(gobs + 2 * i, reinterpret_cast<const float2 *>(src)[i]);
         } else {
-            for (int i = (int)lane; i < n; i += 64) gobs[i] = src[i];
+            for (int i = (int)lane; i < n; i += 64) out_st<kNtRows>(gobs + i, src[i]);
         }
         if (gnorm)
             for (int i = (int)lane; i < n; i += 64) {
@@ -2558,9 +2600,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
         constexpr int SAL = gcd_c(R * 20, 16);
         if (SAL % 16 == 0 && ne == EPW) {
             for (int i = (int)lane; i < n / 4; i += 64)
-                reinterpret_cast<float4 *>(gst)[i] = reinterpret_cast<const float4 *>(st)[i];
+                out_st4<kNtRows>(gst + 4 * i, reinterpret_cast<const float4 *>(st)[i]);
         } else {
-            for (int i = (int)lane; i < n; i += 64) gst[i] = st[i];
+            for (int i = (int)lane; i < n; i += 64) out_st<kNtRows>(gst + i, st[i]);
         }
     }
     STAMP(6);
@@ -2644,8 +2686,8 @@ __device__ __forceinline__ void block_store(float *__restrict__ dst, const float
 {
     const int n4 = n >> 2;
     for (int i = tid; i < n4; i += nt)
-        reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(src)[i];
-    for (int i = (n4 << 2) + tid; i < n; i += nt) dst[i] = src[i];
+        out_st4<kNtRows>(dst + 4 * i, reinterpret_cast<const float4 *>(src)[i]);
+    for (int i = (n4 << 2) + tid; i < n; i += nt) out_st<kNtRows>(dst + i, src[i]);
 }
 
 #ifndef MARLNAV_BLK_EARLY  // 1: stream rows/states out before the per-env phase
@@ -2840,15 +2882,15 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
 #pragma unroll
                 for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
-                b.reward[e] = rsum / (float)A;                     // torch.mean (:233)
+                out_st(&b.reward[e], rsum / (float)A);                     // torch.mean (:233)
 
                 float step_num = lds[BP::SN + l] + 1.0f;           // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
                 const bool terminated = any_col || term_old;       // :213-214
-                b.terminates[e] = (uint8_t)(!term_old && all_in);  // :218-219
-                b.terminated[e] = (uint8_t)terminated;
-                b.truncated[e] = (uint8_t)truncated;
+                out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
+                out_st(&b.terminated[e], (uint8_t)terminated);
+                out_st(&b.truncated[e], (uint8_t)truncated);
                 fin = truncated || terminated;                     // :102-104
                 if ((NOISY || !kBlkSpread) && fin) {  // serial re-init per env
                     KArgsK *kl = kargs_late();
@@ -2888,7 +2930,7 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
                         kl->a.b.target[2 * e + 1] = tgl[1];
                     }
                 }
-                b.step_num[e] = fin ? 0.0f : step_num;
+                out_st(&b.step_num[e], fin ? 0.0f : step_num);
                 tr_l = truncated;
                 co_l = any_col;
                 ta_l = all_in;
