@@ -1264,6 +1264,9 @@ __device__ __forceinline__ MarlnavParams load_params(KArgsK *K)
 // per instruction, then single dwords. src (16-byte aligned) and dst are
 // wave-uniform.
 template <int NB>
+#ifndef MARLNAV_GLDS_AUX  // cache-policy bits of the LDS-DMA staging loads (timing builds)
+#define MARLNAV_GLDS_AUX 0
+#endif
 __device__ __forceinline__ void glds_span(const void *src, float *dst, unsigned lane)
 {
     constexpr int N16 = NB / 16, R4 = (NB % 16) / 4;
@@ -1271,12 +1274,14 @@ __device__ __forceinline__ void glds_span(const void *src, float *dst, unsigned 
     for (int k = 0; k * 64 < N16; ++k) {
         const char *s = in_sgpr(reinterpret_cast<const char *>(src) + k * 1024);
         if ((k + 1) * 64 <= N16 || (int)lane < N16 - k * 64)
-            __builtin_amdgcn_global_load_lds(s + lane * 16u, (LdsVoid *)(dst + k * 256), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(s + lane * 16u, (LdsVoid *)(dst + k * 256), 16, 0,
+                                             MARLNAV_GLDS_AUX);
     }
     if constexpr (R4 > 0) {
         const char *s = in_sgpr(reinterpret_cast<const char *>(src) + N16 * 16);
         if ((int)lane < R4)
-            __builtin_amdgcn_global_load_lds(s + lane * 4u, (LdsVoid *)(dst + N16 * 4), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds(s + lane * 4u, (LdsVoid *)(dst + N16 * 4), 4, 0,
+                                             MARLNAV_GLDS_AUX);
     }
 }
 
