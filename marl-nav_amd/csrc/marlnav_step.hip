@@ -2182,6 +2182,15 @@ struct SplitTerms {
 #define MARLNAV_BLOCK_WPE_ATTR
 #endif
 
+// The target pair takes a spare slot of lane LPR-1 when the other agents (or
+// else the obstacles) do not divide over the LPR lanes: one pair body fewer per
+// wave (A16/O32: 13 -> 12, A3/O8: 4 -> 3); the row leader reads the target
+// angle/distance back from the LDS row.
+template <int A, int O, int LPR>
+constexpr bool kSplitTgtInAg = (A - 1) % LPR != 0;
+template <int A, int O, int LPR>
+constexpr bool kSplitTgtInOb = !kSplitTgtInAg<A, O, LPR> && O % LPR != 0;
+
 // unroll factor of split_pairs' obstacle / other-agent loops (timing builds)
 #ifndef MARLNAV_SPLIT_UNROLL
 #define MARLNAV_SPLIT_UNROLL 64
@@ -2199,9 +2208,10 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
                                                   const MarlnavParams &pr, bool &ok)
 {
     using SP = SplitPlan<A, O, LPR>;
+    constexpr int TQ = LPR - 1;  // the lane whose last other-agent / obstacle slot is spare
     const float cap = pr.cap_distance;
     SplitTerms t{0u, 0, 0.0f, 0.0f};
-    {
+    if constexpr (!kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>) {
         const float d = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
         const float ang = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, d, cap, ok);
         t.ta = ang;
@@ -2214,33 +2224,56 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     MARLNAV_UNROLL(MARLNAV_SPLIT_UNROLL)
     for (int i = 0; i < SP::NOB; ++i) {
         const int j = q + LPR * i;
-        if (O % LPR == 0 || j < O) {
-            const float px = obe[2 * j], py = obe[2 * j + 1];
+        constexpr bool spare = kSplitTgtInOb<A, O, LPR>;
+        const bool last = i == SP::NOB - 1;
+        const bool valid = O % LPR == 0 || j < O;
+        const bool tgt = spare && last && q == TQ;  // j >= O there: the target pair
+        if (valid || tgt) {
+            const float *pt = tgt ? tge : obe + 2 * (valid ? j : 0);
+            const float px = pt[0], py = pt[1];
             const float d = pair_dist<FAST>(ox, oy, px, py, ok);
-            orow[2 + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
-            orow[2 + O + j] = d;
-            if (TERMS)
-                t.fl |= (d < pr.ob_risk_dist ? 1u : 0u) | (d < pr.ob_coll_dist ? 2u : 0u);
+            const float ang = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
+            if (valid) {
+                orow[2 + j] = ang;
+                orow[2 + O + j] = d;
+                if (TERMS)
+                    t.fl |= (d < pr.ob_risk_dist ? 1u : 0u) | (d < pr.ob_coll_dist ? 2u : 0u);
+            } else {
+                orow[0] = ang;
+                orow[1] = d;
+            }
         }
     }
     MARLNAV_UNROLL(MARLNAV_SPLIT_UNROLL)
     for (int i = 0; i < SP::NAG; ++i) {
         const int kx = q + LPR * i;  // index among the others
-        if ((A - 1) % LPR == 0 || kx < A - 1) {
-            const int m = kx + (kx >= a ? 1 : 0);
-            const float px = sts[5 * m], py = sts[5 * m + 1];
+        constexpr bool spare = kSplitTgtInAg<A, O, LPR>;
+        const bool last = i == SP::NAG - 1;
+        const bool valid = (A - 1) % LPR == 0 || kx < A - 1;
+        const bool tgt = spare && last && q == TQ;  // kx >= A - 1 there: the target pair
+        if (valid || tgt) {
+            const int m = valid ? kx + (kx >= a ? 1 : 0) : 0;
+            const float *pt = tgt ? tge : sts + 5 * m;
+            const float px = pt[0], py = pt[1];
             const float d = pair_dist<FAST>(ox, oy, px, py, ok);
-            orow[2 + 2 * O + kx] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
-            orow[2 + 2 * O + (A - 1) + kx] = d;
-            if (TERMS) {
-                t.fl |= (d < pr.ag_risk_dist ? 4u : 0u) | (d < pr.ag_coll_dist ? 8u : 0u);
-                t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
-                if constexpr (FAST && MARLNAV_FM_TERMS) {
-                    const float sd = div_c(d - pr.ideal_dist, make_divc(pr.bond_sharpness, ok), ok);
-                    bond_row[kx] = recip_fast(1.0f + sd * sd, ok);
-                } else {
-                    const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
-                    bond_row[kx] = 1.0f / (1.0f + sd * sd);
+            const float ang = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
+            if (!valid) {
+                orow[0] = ang;
+                orow[1] = d;
+            } else {
+                orow[2 + 2 * O + kx] = ang;
+                orow[2 + 2 * O + (A - 1) + kx] = d;
+                if (TERMS) {
+                    t.fl |= (d < pr.ag_risk_dist ? 4u : 0u) | (d < pr.ag_coll_dist ? 8u : 0u);
+                    t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
+                    if constexpr (FAST && MARLNAV_FM_TERMS) {
+                        const float sd =
+                            div_c(d - pr.ideal_dist, make_divc(pr.bond_sharpness, ok), ok);
+                        bond_row[kx] = recip_fast(1.0f + sd * sd, ok);
+                    } else {
+                        const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
+                        bond_row[kx] = 1.0f / (1.0f + sd * sd);
+                    }
                 }
             }
         }
@@ -2371,6 +2404,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
             const int band = lpr_sum<LPR>(t.band);
             wave_sync();  // bond terms of the row are in LDS
             if (row_on && q == 0) {
+                if constexpr (kSplitTgtInAg<A, O, LPR> || kSplitTgtInOb<A, O, LPR>) {
+                    t.ta = orow[0];  // computed by lane LPR-1 (wave_sync above)
+                    t.td = orow[1];
+                }
                 const float head = fabsf(t.ta) < pr.max_angle_diff ? 1.0f : 0.0f;
                 const float bandf = (float)band;
                 const float bandc = bandf < pr.max_at_prop_d ? bandf : pr.max_at_prop_d;
