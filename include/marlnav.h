@@ -167,6 +167,22 @@ int marlnav_discounted_returns(const float *rewards, const uint8_t *done, int64_
                                int64_t P, double gamma, double *returns, double *stats,
                                double *work, void *stream);
 
+/* Testing hook (not part of the reference's interface): restrict the step /
+ * observe kernel selection to one family, process-wide. 0 = automatic (the
+ * default); a family that does not support the call's shape or buffer
+ * alignment falls back to the generic wave kernel. Returns the previous
+ * setting. */
+#define MARLNAV_FAMILY_AUTO 0
+#define MARLNAV_FAMILY_BLOCK 1 /* env-block kernel (compiled shapes)          */
+#define MARLNAV_FAMILY_SPLIT 2 /* pair-split kernel (compiled shapes)         */
+#define MARLNAV_FAMILY_TILE 3  /* wave-tile kernel (compiled shapes)          */
+#define MARLNAV_FAMILY_WAVE 4  /* generic wave kernel (any shape)             */
+int marlnav_debug_force_family(int family);
+
+/* Family (MARLNAV_FAMILY_*) the last marlnav_step / marlnav_observe call on
+ * this thread launched. */
+int marlnav_debug_last_family(void);
+
 /* Message of the last failing call on this thread. */
 const char *marlnav_last_error(void);
 

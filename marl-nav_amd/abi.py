@@ -63,7 +63,8 @@ class MarlnavStepBuffers(ctypes.Structure):
 EXPORTS = ("marlnav_step", "marlnav_observe", "marlnav_reinit_all",
            "marlnav_counter_slots", "marlnav_counters_total",
            "marlnav_returns_work_size", "marlnav_discounted_returns",
-           "marlnav_last_error", "marlnav_abi_version")
+           "marlnav_last_error", "marlnav_abi_version",
+           "marlnav_debug_force_family", "marlnav_debug_last_family")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmarlnav.so")
@@ -93,6 +94,10 @@ def _declare(lib):
     lib.marlnav_last_error.restype = c.c_char_p
     lib.marlnav_abi_version.argtypes = []
     lib.marlnav_abi_version.restype = c.c_int
+    lib.marlnav_debug_force_family.argtypes = [c.c_int]
+    lib.marlnav_debug_force_family.restype = c.c_int
+    lib.marlnav_debug_last_family.argtypes = []
+    lib.marlnav_debug_last_family.restype = c.c_int
     return lib
 
 

@@ -3264,7 +3264,8 @@ const SplitVariant kSplitVariants[] = {
 // 16384x3x3 does not)
 constexpr int64_t kSplitBelowWaves = 512;
 
-const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only)
+const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only,
+                                 bool force_size = false)
 {
     static const int forced = [] {
         const char *v = getenv("MARLNAV_SPLIT");
@@ -3277,7 +3278,8 @@ const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers 
     if (!v) return nullptr;
     const int64_t row_waves = (d->num_parallel + tile_envs(v->A) - 1) / tile_envs(v->A);
     const int64_t pairs = 1 + v->O + (v->A - 1);
-    if (!v->always && forced != 1 && row_waves * 6 >= kSplitBelowWaves * pairs) return nullptr;
+    if (!v->always && forced != 1 && !force_size && row_waves * 6 >= kSplitBelowWaves * pairs)
+        return nullptr;
     if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
         !aligned(b.obs, 16))
         return nullptr;
@@ -3419,11 +3421,28 @@ int launch(StepFn fn, const Launch &L, StepArgs args, MarlnavParams pr, void *st
     return 0;
 }
 
+// marlnav_debug_force_family / marlnav_debug_last_family (testing hooks)
+int g_family = MARLNAV_FAMILY_AUTO;
+thread_local int g_last_family = MARLNAV_FAMILY_AUTO;
+
+bool family_allowed(int f) { return g_family == MARLNAV_FAMILY_AUTO || g_family == f; }
+
 }  // namespace
 
 extern "C" {
 
 int marlnav_abi_version(void) { return MARLNAV_ABI_VERSION; }
+
+int marlnav_debug_force_family(int family)
+{
+    const int prev = g_family;
+    if (family < MARLNAV_FAMILY_AUTO || family > MARLNAV_FAMILY_WAVE)
+        return fail(MARLNAV_EINVAL, "unknown kernel family %d", family);
+    g_family = family;
+    return prev;
+}
+
+int marlnav_debug_last_family(void) { return g_last_family; }
 
 #if MARLNAV_STAMPS
 int marlnav_debug_stamps(void *buf)
@@ -3462,17 +3481,27 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavSte
     args.b = *b;
     args.step_idx = step_idx;
     const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
-    if (const SplitVariant *v = select_split(d, *b, false))
-        return launch_split(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
-    if (const BlockVariant *v = select_block(d, *b, false))
-        return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
-    if (const TilePair *t = select_tile(d, *b, false)) {
-        const int r = pick_rpl(d->num_parallel, d->num_agents);
-        const TileSet &ts = t->rpl[r - 1];
-        return launch_tile(noisy ? ts.noisy : ts.step, ts.lds, r, L, args, *pr, stream,
-                           "marlnav_step");
-    }
+    const bool fsplit = g_family == MARLNAV_FAMILY_SPLIT;
+    if (family_allowed(MARLNAV_FAMILY_SPLIT))
+        if (const SplitVariant *v = select_split(d, *b, false, fsplit)) {
+            g_last_family = MARLNAV_FAMILY_SPLIT;
+            return launch_split(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
+        }
+    if (family_allowed(MARLNAV_FAMILY_BLOCK))
+        if (const BlockVariant *v = select_block(d, *b, false)) {
+            g_last_family = MARLNAV_FAMILY_BLOCK;
+            return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
+        }
+    if (family_allowed(MARLNAV_FAMILY_TILE))
+        if (const TilePair *t = select_tile(d, *b, false)) {
+            const int r = pick_rpl(d->num_parallel, d->num_agents);
+            const TileSet &ts = t->rpl[r - 1];
+            g_last_family = MARLNAV_FAMILY_TILE;
+            return launch_tile(noisy ? ts.noisy : ts.step, ts.lds, r, L, args, *pr, stream,
+                               "marlnav_step");
+        }
     const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
+    g_last_family = MARLNAV_FAMILY_WAVE;
     return launch(noisy ? k.noisy : k.step, L, args, *pr, stream, "marlnav_step");
 }
 
@@ -3491,15 +3520,25 @@ int marlnav_observe(const MarlnavDims *d, const float *states, const float *obst
     MarlnavParams pr;
     memset(&pr, 0, sizeof(pr));
     pr.cap_distance = 0.1f;  // environment.py:65
-    if (const SplitVariant *v = select_split(d, args.b, true))
-        return launch_split(*v, v->obs, args, pr, stream, "marlnav_observe");
-    if (const BlockVariant *v = select_block(d, args.b, true))
-        return launch_block(*v, v->obs, args, pr, stream, "marlnav_observe");
-    if (const TilePair *t = select_tile(d, args.b, true)) {
-        const int r = pick_rpl(d->num_parallel, d->num_agents);
-        return launch_tile(t->rpl[r - 1].obs, t->rpl[r - 1].lds, r, L, args, pr, stream,
-                           "marlnav_observe");
-    }
+    const bool fsplit = g_family == MARLNAV_FAMILY_SPLIT;
+    if (family_allowed(MARLNAV_FAMILY_SPLIT))
+        if (const SplitVariant *v = select_split(d, args.b, true, fsplit)) {
+            g_last_family = MARLNAV_FAMILY_SPLIT;
+            return launch_split(*v, v->obs, args, pr, stream, "marlnav_observe");
+        }
+    if (family_allowed(MARLNAV_FAMILY_BLOCK))
+        if (const BlockVariant *v = select_block(d, args.b, true)) {
+            g_last_family = MARLNAV_FAMILY_BLOCK;
+            return launch_block(*v, v->obs, args, pr, stream, "marlnav_observe");
+        }
+    if (family_allowed(MARLNAV_FAMILY_TILE))
+        if (const TilePair *t = select_tile(d, args.b, true)) {
+            const int r = pick_rpl(d->num_parallel, d->num_agents);
+            g_last_family = MARLNAV_FAMILY_TILE;
+            return launch_tile(t->rpl[r - 1].obs, t->rpl[r - 1].lds, r, L, args, pr, stream,
+                               "marlnav_observe");
+        }
+    g_last_family = MARLNAV_FAMILY_WAVE;
     return launch(select_kernels(d->num_agents, d->num_obstacles).obs, L, args, pr, stream,
                   "marlnav_observe");
 }

@@ -546,3 +546,64 @@ def test_native_noisy_agents_bit_exact_vs_oracle(pkg, P, A, O):
         assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, where=where)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                "terminates"))
+
+
+FAMILIES = {1: "block", 2: "split", 3: "tile", 4: "wave"}
+
+
+@pytest.mark.parametrize("P,A,O,expect", [
+    (4096 + 5, 3, 3, {1, 2, 3, 4}),   # every family holds the A3/O3 shape
+    (2048 + 3, 3, 8, {1, 2, 3, 4}),
+    (5000 + 1, 2, 1, {1, 3, 4}),      # no split variant at A2/O1
+    (200, 16, 32, {2, 4}),            # split (compiled) or the generic wave kernel
+    (777, 5, 2, {4}),                 # runtime shape: wave kernel only
+])
+def test_every_kernel_family_bit_exact_vs_oracle(pkg, P, A, O, expect):
+    """The host picks one of four kernel families by shape and grid size
+    (DESIGN.md §3); the automatic choice leaves some of them unused at the
+    sizes above. Force each in turn (marlnav_debug_force_family) over the
+    same seeded trajectory - native re-init, 3-step episodes, the observe-only
+    instantiation through Env.observations() - and check each against the
+    oracle bit for bit (angles within the acosf budget)."""
+    ran = set()
+    for fam in FAMILIES:
+        g = torch.Generator().manual_seed(P + A + O)
+        env = make_env(pkg, P, A, O, episode_len=3, seed=21,
+                       factors=dict(risk_factor=3., distance_factor=7., bond_factor=2.))
+        lib = env._lib
+        prev = lib.marlnav_debug_force_family(fam)
+        try:
+            dm, pr = oracle_params(env)
+            form = np_(env._formation)
+            st, ob, tg = orc.reinit_all(dm, pr, form, 0)
+            sn = np.zeros(P, np.float32)
+            te = np.zeros(P, np.bool_)
+            for k in range(4):
+                acts = ((torch.rand(P, A, 2, generator=g) - 0.5) * 0.8).numpy()
+                exp = orc.step(dm, pr, st, ob, tg, sn, te, acts, formation=form,
+                               step_idx=k + 1)
+                obs, rew, term, trunc = env.step(torch.from_numpy(acts).to(DEV))
+                torch.cuda.synchronize()
+                got_fam = lib.marlnav_debug_last_family()
+                where = f"P{P} A{A} O{O} forced {FAMILIES[fam]} ran {FAMILIES[got_fam]} step {k + 1}"
+                for name, got in (("states", env.states), ("obstacles", env.obstacles),
+                                  ("target", env.target), ("step_num", env._step_num),
+                                  ("terminates", env._terminates), ("reward", rew),
+                                  ("terminated", term), ("truncated", trunc)):
+                    np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
+                fg = orc.split_obs(np_(obs._packed), A, O)
+                fo = orc.split_obs(exp["obs"], A, O)
+                assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7,
+                                 where=where)
+                st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target",
+                                                       "step_num", "terminates"))
+            ran.add(got_fam)
+            o2 = env.observations()  # observe-only instantiation of the same family
+            torch.cuda.synchronize()
+            assert lib.marlnav_debug_last_family() == got_fam
+            fg = orc.split_obs(np_(o2._packed), A, O)
+            assert_obs_close(fg, dict(zip(OBS_FIELDS, orc.split_obs(exp["obs"], A, O))),
+                             prefix="", rtol=5e-7, where=where + " observe")
+        finally:
+            lib.marlnav_debug_force_family(prev)
+    assert ran == expect, (sorted(ran), sorted(expect))
