@@ -16,11 +16,13 @@ Timing: W untimed steps; barrier + synchronize; K timed steps; synchronize +
 barrier; the max over ranks. value = N*P*K / max time.
 
 roofline: the step kernel's average duration from HIP events recorded on the
-launch stream around replays of a hipGraph of back-to-back Env.step launches
-(so no kernel waits on Python; the graph's inter-kernel gap is included), against the
-algorithmic bytes per env-step (read 28A+8O+13, write 20A+4A*D+11: 336 B at
-A3/O3) and the 8 TB/s HBM peak. traffic: HBM bytes per launch from the
-committed rocprofv3 PMC summary for this config (profiles/), or null.
+launch stream (torch's current stream, where Env.step enqueues) around the
+timed region, divided by K (an upper bound: inter-kernel gaps are included),
+against the algorithmic bytes per env-step (read 28A+8O+13, write
+20A+4A*D+11: 336 B at A3/O3) and the 8 TB/s HBM peak. kernel_us_graph: the
+same from replays of a hipGraph of back-to-back Env.step launches, for
+reference. traffic: HBM bytes per launch from the committed rocprofv3 PMC
+summary for this config (profiles/), or null.
 
 cpu_baseline (rank 0, N=1): oracle/torch_ref.py - the reference's step
 restated with its own execution structure in eager PyTorch on the host CPU -
@@ -184,15 +186,20 @@ def main():
 
     barrier()
     torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for i in range(a.steps):
         env.step(actions[i % len(actions)])
+    ev1.record()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
     dt = pkg.shard.max_over_ranks(dt, red_dev)
+    kern_avg = ev0.elapsed_time(ev1) * 1e3 / a.steps  # us per step-kernel, timed region
 
-    kern_avg, kern_med = kernel_time_us(env, actions)
+    kern_graph, kern_med = kernel_time_us(env, actions)
     per_env = alg_bytes_per_env(A, O)
     launch_bytes = per_env * P
     achieved = launch_bytes / (kern_avg * 1e-6) / 1e9
@@ -233,7 +240,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel_us_avg": kern_avg, "kernel_us_median": kern_med,
+                         "kernel_us_avg": kern_avg, "kernel_us_graph": kern_graph,
+                         "kernel_us_graph_median": kern_med,
                          "alg_bytes_per_launch": launch_bytes,
                          "alg_bytes_per_env_step": per_env},
             "cpu_baseline": cpu,

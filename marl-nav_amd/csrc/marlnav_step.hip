@@ -2699,7 +2699,8 @@ struct BlockPlan {
     static constexpr int OBS = RED + 4 * R;                // (R, D) packed rows
     static constexpr int LIST = (OBS + R * D + 3) & ~3;    // (E,) finished envs
     static constexpr int FLG = LIST + E;                   // [0] nfin, [1 + w] wave w coords bad
-    static constexpr int FLOATS = (FLG + 1 + A + 3) & ~3;
+    static constexpr int LIST2 = (FLG + 1 + A + 3) & ~3;   // (A-1, E) finished envs, waves >= 1
+    static constexpr int FLOATS = (LIST2 + (A - 1) * E + 3) & ~3;
     static_assert(A >= 2 && A <= 16, "one wave per agent");
 };
 
@@ -2740,6 +2741,10 @@ __device__ __forceinline__ void block_store(float *__restrict__ dst, const float
 #endif
 constexpr bool kBlkEarly = MARLNAV_BLK_EARLY != 0;
 constexpr bool kBlkSpread = MARLNAV_BLK_SPREAD != 0;
+#ifndef MARLNAV_BLK_OVERLAP  // 1: waves 1..A-1 re-init finished envs during the per-env phase
+#define MARLNAV_BLK_OVERLAP 1
+#endif
+constexpr bool kBlkOverlap = MARLNAV_BLK_OVERLAP != 0 && kBlkSpread && !kBlkEarly;
 
 // Phases (one block barrier after each): stage | move + coordinate check
 // (moved states start streaming out) | observe into LDS rows | rows stream
@@ -2904,6 +2909,10 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
     if (!OBS_ONLY) {
         int *list = reinterpret_cast<int *>(lds + BP::LIST);
         int *flg = reinterpret_cast<int *>(lds + BP::FLG);
+        const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
+        // native (non-noisy) re-init: waves 1..A-1 take the finished envs
+        // while wave 0 runs the per-env phase (below)
+        const bool overlap = !NOISY && kBlkOverlap && !kargs_late()->a.b.fresh_states;
         // ---- per-env reductions, terminal logic (wave 0, one lane per env)
         if (w == 0) {
             const bool env_on = l < ne;
@@ -2998,15 +3007,38 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
                     }
                 }
             }
+        } else if (overlap) {
+            // ---- waves 1..A-1, while wave 0 runs the per-env phase: the
+            // finished set from the inputs wave 0 uses (red flags, step_num,
+            // terminates), then the native re-init (:104) and re-observation
+            // (:105) of those envs. Disjoint LDS: wave 0 reads red/SN/TM; this
+            // writes the states, obstacles, target and rows of finished envs.
+            bool fin = false;
+            if (l < ne) {
+                unsigned any_col = 0u;
+#pragma unroll
+                for (int i = 0; i < A; ++i) any_col |= __float_as_uint(red[A * l + i].z) & 1u;
+                fin = lds[BP::SN + l] + 1.0f > pr.trunc_after || any_col != 0u ||
+                      reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
+            }
+            const uint64_t fm = __ballot(fin);
+            if (fm) {
+                int *wlist = reinterpret_cast<int *>(lds + BP::LIST2) + E * (w - 1);
+                if (fin)
+                    wlist[__builtin_amdgcn_mbcnt_hi(
+                        (unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] = l;
+                wave_sync();  // every lane of this wave sees its list
+                reinit_reobs_native<A, O>(kargs_late(), ev, lds + BP::FORM, wlist,
+                                          (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
+            }
         }
         __syncthreads();
         STAMP(4);
         const int nfin = flg[0];
-        if (nfin) {
+        if (nfin && !overlap) {
             // ---- masked re-init (:104) and observations of the re-initialised
             // envs (:105), then their rows and states go out again
             KArgsK *kl = kargs_late();
-            const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
             if (!NOISY && kBlkSpread && !kl->a.b.fresh_states) {
                 reinit_reobs_native<A, O>(kl, ev, lds + BP::FORM, list, nfin, pr.cap_distance,
                                           tid, NT);
