@@ -388,8 +388,10 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
 {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
-        const uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
+        // one v_mad_u64_u32 per product instead of v_mul_lo_u32 + v_mul_hi_u32
+        const uint64_t p0 = (uint64_t)c[0] * 0xD2511F53u, p1 = (uint64_t)c[2] * 0xCD9E8D57u;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
         c[0] = n0;
         c[1] = lo1;
