@@ -3273,13 +3273,14 @@ struct SplitVariant {
     TileFn step, obs, noisy;
     size_t lds;
     bool always;  // also for large grids
+    int lpr;
 };
 
 #define MARLNAV_SPLIT_VARIANT(A, O, LPR, ALWAYS)                                          \
     {A, O, SplitPlan<A, O, LPR>::EPW, split_kernel<A, O, LPR, false, false>,             \
      split_kernel<A, O, LPR, true, false>, split_kernel<A, O, LPR, false, true>,         \
      (size_t)(SplitPlan<A, O, LPR>::FLOATS * kWavesPerBlock + SplitPlan<A, O, LPR>::BLK) * 4, \
-     ALWAYS}
+     ALWAYS, LPR}
 const SplitVariant kSplitVariants[] = {
 #ifndef MARLNAV_C4_LPR  // lanes per agent row at A16/O32 (timing builds)
 #define MARLNAV_C4_LPR 4
@@ -3290,7 +3291,13 @@ const SplitVariant kSplitVariants[] = {
 #ifdef MARLNAV_SPLIT33_LPR2
     MARLNAV_SPLIT_VARIANT(3, 3, 2, false),
 #endif
+    // 8 lanes per row (<= 2 pairs per lane) for grids of at most kSplitTinyWaves
+    // LPR=4 waves (measured: 2x3x3 3.89 -> 3.44 us, 1024x3x8 6.31 -> 6.14 us;
+    // 2048x3x3 and 4096x3x3 slower)
+    MARLNAV_SPLIT_VARIANT(3, 8, 8, false),
+    MARLNAV_SPLIT_VARIANT(3, 3, 8, false),
 };
+constexpr int64_t kSplitTinyWaves = 256;
 #undef MARLNAV_SPLIT_VARIANT
 
 // one-lane-per-row grids below kSplitBelowWaves * (pairs per row / 6) waves
@@ -3307,8 +3314,14 @@ const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers 
     }();
     if (forced == 0 || d->obstacle_stride != d->num_obstacles) return nullptr;
     const SplitVariant *v = nullptr;
-    for (const SplitVariant &x : kSplitVariants)
-        if (x.A == d->num_agents && x.O == d->num_obstacles) v = &x;
+    for (const SplitVariant &x : kSplitVariants) {
+        if (x.A != d->num_agents || x.O != d->num_obstacles) continue;
+        if (x.lpr == 8) {  // the tiny-grid form: LPR=4 would leave >3/4 of the SIMDs idle
+            const int64_t e4 = 64 / 4 / x.A;
+            if ((d->num_parallel + e4 - 1) / e4 > kSplitTinyWaves) continue;
+        }
+        v = &x;  // the last applicable variant wins
+    }
     if (!v) return nullptr;
     const int64_t row_waves = (d->num_parallel + tile_envs(v->A) - 1) / tile_envs(v->A);
     const int64_t pairs = 1 + v->O + (v->A - 1);
