@@ -2747,6 +2747,10 @@ constexpr bool kBlkSpread = MARLNAV_BLK_SPREAD != 0;
 #define MARLNAV_BLK_OVERLAP 1
 #endif
 constexpr bool kBlkOverlap = MARLNAV_BLK_OVERLAP != 0 && kBlkSpread && !kBlkEarly;
+#ifndef MARLNAV_BLK_PRIO  // s_setprio level of blocks with finished envs (0: off)
+#define MARLNAV_BLK_PRIO 0
+#endif
+constexpr int kBlkPrio = MARLNAV_BLK_PRIO;
 
 // Phases (one block barrier after each): stage | move + coordinate check
 // (moved states start streaming out) | observe into LDS rows | rows stream
@@ -2989,6 +2993,7 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
                 ta_l = all_in;
             }
             const uint64_t finmask = __ballot(fin);
+            if (kBlkPrio && finmask) __builtin_amdgcn_s_setprio(kBlkPrio);
             if (fin)
                 list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
                                                __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] = l;
@@ -3025,6 +3030,9 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
             }
             const uint64_t fm = __ballot(fin);
             if (fm) {
+                // this block now sets the kernel's end: its waves go first on
+                // their SIMDs (the other blocks there have slack)
+                if (kBlkPrio) __builtin_amdgcn_s_setprio(kBlkPrio);
                 int *wlist = reinterpret_cast<int *>(lds + BP::LIST2) + E * (w - 1);
                 if (fin)
                     wlist[__builtin_amdgcn_mbcnt_hi(
