@@ -188,6 +188,24 @@ __device__ __forceinline__ bool mag_ok(float x, float lo, float hi)
 // [2^-43, 2^41] (div2_fast guard [2^-60, 2^60]).
 __device__ __forceinline__ bool coord_ok(float c) { return mag_ok(c, 0x1p-20f, 0x1p40f); }
 
+// coord_ok over many values without per-value compares: |c| as bits is
+// monotone for non-negative floats, so accumulate min(bits - 1) (0 wraps to
+// the largest value: zero passes) and max(bits) (NaN and inf exceed 2^40),
+// then compare once. Equal to AND over coord_ok.
+struct CoordRange {
+    uint32_t lo = 0xffffffffu, hi = 0u;
+    __device__ void add(float c)
+    {
+        const uint32_t u = __float_as_uint(c) & 0x7fffffffu;
+        lo = u - 1u < lo ? u - 1u : lo;
+        hi = u > hi ? u : hi;
+    }
+    __device__ bool ok() const
+    {
+        return lo >= __float_as_uint(0x1p-20f) - 1u && hi <= __float_as_uint(0x1p40f);
+    }
+};
+
 // coord_ok over a full tile's staged obstacle (NOB floats) and target (NTG)
 // coordinates, spread over the wave's lanes
 template <int NOB, int NTG>
@@ -2811,9 +2829,25 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
     const int r = l * A + w;  // row of this lane
     const bool row_on = l < ne;
     const int nrow = ne * A;
+    int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
+    if (tid == 0) *bad_word = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
     __syncthreads();
     STAMP(1);
+
+    // obstacle and target coordinates of the block for the pair-math choice
+    // (below); read before the move writes LDS, so the reads overlap it
+    // (a partial last block takes the IEEE path without checking)
+    CoordRange crange;
+    if (!(MARLNAV_ABLATE & 128) && full) {
+        constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
+        static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
+#pragma unroll
+        for (int k2 = 0; k2 * NT < NC; ++k2) {
+            const int i = tid + k2 * NT;
+            if ((k2 + 1) * NT <= NC || i < NC) crange.add(lds[BP::OB + i]);
+        }
+    }
 
     // ---- _move_agents (environment.py:113-123), own row in registers
     float ox, oy, dx, dy;
@@ -2853,30 +2887,21 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
     }
     // block-uniform choice of the pair math: the short sqrt / shared-
     // reciprocal division (equal to IEEE there) when every coordinate of the
-    // block passes coord_ok, IEEE otherwise
-    {
-        bool cok = !row_on || (coord_ok(ox) && coord_ok(oy));
-        constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
-        static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
-#pragma unroll
-        for (int k2 = 0; k2 * NT < NC; ++k2) {
-            const int i = tid + k2 * NT;
-            if ((k2 + 1) * NT <= NC || i < NC) {
-                const bool used =
-                    full || (i < E * O * 2 ? i / (O * 2) < ne : (i - E * O * 2) / 2 < ne);
-                cok = cok && (!used || coord_ok(lds[BP::OB + i]));
-            }
-        }
-        const bool bad = __ballot(!cok) != 0ull;
-        if (lane == 0) reinterpret_cast<int *>(lds + BP::FLG)[1 + w] = bad ? 1 : 0;
+    // block (obstacles and targets above, moved agents here) passes coord_ok,
+    // IEEE otherwise
+    if (!(MARLNAV_ABLATE & 128) && full) {
+        crange.add(ox);
+        crange.add(oy);
+        // one word for the block, written only by waves that found one (all
+        // write 1: a benign race); read once after the barrier
+        const bool bad = __ballot(!crange.ok()) != 0ull;
+        if (lane == 0 && bad) *bad_word = 1;
     }
     __syncthreads();
     STAMP(2);
     // the moved states are final except in finished envs (re-stored below)
     if (kBlkEarly && !OBS_ONLY) block_store(in_sgpr(b.states + e0 * (A * 5)), st, nrow * 5, tid, NT);
-    bool fast = full;
-#pragma unroll
-    for (int q = 0; q < A; ++q) fast = fast && reinterpret_cast<const int *>(lds + BP::FLG)[1 + q] == 0;
+    const bool fast = full && ((MARLNAV_ABLATE & 128) || *bad_word == 0);  // 128: timing only
 
     // ---- observations of the moved state + reward terms (:99-100)
     float4 *red = reinterpret_cast<float4 *>(lds + BP::RED);
