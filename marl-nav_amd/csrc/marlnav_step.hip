@@ -165,6 +165,12 @@ constexpr bool kGuardedFast = false;
 #ifndef MARLNAV_FM_TERMS
 #define MARLNAV_FM_TERMS 0
 #endif
+// Internal MarlnavParams.flags bit set by marlnav_step when every reward
+// parameter lies inside the short division sequences' guards
+// (terms_fast_params): the observe_row_own reward terms then use them in
+// FAST (coordinate-checked) waves. Never set by callers (above the public
+// MARLNAV_* flag bits).
+constexpr uint32_t kTermsFastFlag = 1u << 30;
 
 // x == 0 or x = m * 2^e with e in [-59, 62] (|x| in [2^-60, 2^62)); NaN and
 // infinities pass (they also fail the denominators' guard)
@@ -839,18 +845,21 @@ __device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
         const float ideal = pr.ideal_dist, sharp = pr.bond_sharpness;
         const float bandc = band < pr.max_at_prop_d ? band : pr.max_at_prop_d;
         float dsc, soft, bondm;
-        if constexpr (FAST && MARLNAV_FM_TERMS) {
+        if (FAST && (MARLNAV_FM_TERMS || (pr.flags & kTermsFastFlag))) {
+            // exact: the host set kTermsFastFlag only for parameters inside
+            // the div_c / recip_fast guards (terms_fast_params), and FAST
+            // coordinates bound every distance (coord_ok), so every operand
+            // below stays in range
             const DivC d_mapd = make_divc(pr.max_at_prop_d, ok);
             const DivC d_init = make_divc(pr.init_dist, ok);
             const DivC d_sharp = make_divc(sharp, ok);
-            const DivC d_am1 = make_divc((float)(A - 1), ok);
             dsc = div_c(bandc, d_mapd, ok);
             soft = -1.0f * div_c(td, d_init, ok);
             const float bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [&](float d) {
                 const float sd = div_c(d - ideal, d_sharp, ok);
                 return recip_fast(1.0f + sd * sd, ok);
             });
-            bondm = div_c(bond, d_am1, ok);
+            bondm = bond / (float)(A - 1);  // the bond sum can be tiny: IEEE
         } else {
             dsc = bandc / pr.max_at_prop_d;
             soft = -1.0f * (td / pr.init_dist);
@@ -3540,9 +3549,33 @@ int64_t marlnav_counter_slots(const MarlnavDims *d)
     return plan_launch(d).waves;
 }
 
-int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr, const MarlnavStepBuffers *b,
+namespace {
+// Parameter ranges under which the reward terms' divisions by bond_sharpness,
+// init_dist and max_at_prop_d (div_c) and the bond reciprocal (recip_fast)
+// are exact for every FAST-range distance: divisors in [2^-20, 2^20] (the
+// sharpness in [2^-5, 2^20], so |(d - ideal) / sharpness| <= 2^48 and
+// 1 + sd^2 <= 2^96), ideal_dist zero or in [2^-40, 2^40] (so d - ideal is
+// zero or >= 2^-66 in magnitude).
+bool terms_fast_params(const MarlnavParams &p)
+{
+    const auto in = [](float c, float lo, float hi) {
+        const float a = fabsf(c);
+        return a >= lo && a <= hi;
+    };
+    return in(p.bond_sharpness, 0x1p-5f, 0x1p20f) && in(p.init_dist, 0x1p-20f, 0x1p20f) &&
+           in(p.max_at_prop_d, 0x1p-20f, 0x1p20f) &&
+           (p.ideal_dist == 0.0f || in(p.ideal_dist, 0x1p-40f, 0x1p40f));
+}
+}  // namespace
+
+int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const MarlnavStepBuffers *b,
                  uint64_t step_idx, void *stream)
 {
+    if (!pr_in) return fail(MARLNAV_EINVAL, "params/buffers is NULL");
+    MarlnavParams prm = *pr_in;
+    prm.flags &= ~kTermsFastFlag;
+    if (terms_fast_params(prm)) prm.flags |= kTermsFastFlag;
+    const MarlnavParams *pr = &prm;
     if (int rc = validate(d)) return rc;
     if (!pr || !b) return fail(MARLNAV_EINVAL, "params/buffers is NULL");
     if (!b->states || !b->obstacles || !b->target || !b->step_num || !b->terminates ||
