@@ -607,3 +607,37 @@ def test_every_kernel_family_bit_exact_vs_oracle(pkg, P, A, O, expect):
         finally:
             lib.marlnav_debug_force_family(prev)
     assert ran == expect, (sorted(ran), sorted(expect))
+
+
+@pytest.mark.parametrize("geom", [
+    dict(_init_dist=7.0, _bond_sharpness=0.05, _ideal_dist=33.3, _max_at_prop_d=3),  # fast terms
+    dict(_init_dist=3.0e7, _bond_sharpness=0.01, _ideal_dist=1e-30),                   # IEEE terms
+    dict(_bond_sharpness=1e6, _ideal_dist=0.0, _max_at_prop_d=1.5e-6),                 # boundaries
+])
+def test_reward_term_divisions_bit_exact_for_any_parameters(pkg, geom):
+    """The reward terms divide by parameters (environment.py:236-269); the
+    kernels use the short exact division sequences only when the host finds
+    every such parameter inside their guards (marlnav_step, terms_fast_params)
+    and IEEE division otherwise. Rewards stay bit-exact vs the oracle
+    (which divides with IEEE division) either way."""
+    P, A, O = 20000 + 3, 3, 3
+    g = torch.Generator().manual_seed(77)
+    env = make_env(pkg, P, A, O, episode_len=40, seed=3,
+                   factors=dict(risk_factor=1.5, distance_factor=3., soft_factor=7.,
+                                bond_factor=11.))
+    for k, v in geom.items():
+        setattr(env, k, v)
+    dm, pr = oracle_params(env)
+    form = np_(env._formation)
+    st, ob, tg = (np_(x).copy() for x in (env.states, env.obstacles, env.target))
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    for k in range(4):
+        acts = ((torch.rand(P, A, 2, generator=g) - 0.5) * 0.8).numpy()
+        exp = orc.step(dm, pr, st, ob, tg, sn, te, acts, formation=form, step_idx=k + 1)
+        obs, rew, term, trunc = env.step(torch.from_numpy(acts).to(DEV))
+        where = f"{geom} step {k + 1}"
+        np.testing.assert_array_equal(np_(rew), exp["reward"], where)
+        np.testing.assert_array_equal(np_(env.states), exp["states"], where)
+        st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
+                                               "terminates"))
