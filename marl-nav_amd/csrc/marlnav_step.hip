@@ -1463,9 +1463,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
     const int64_t tile = gw;
     KArgsK *K = kargs_late();
     const int64_t P = K->a.P;
+    // pointers first: one round of kernarg loads ahead of the first wait
+    const StepPtrs b = load_ptrs(K);
     if (tile >= K->a.ntiles) return;
     STAMP(0);
-    const StepPtrs b = load_ptrs(K);
     float *wl = lds + wib * TP::FLOATS;
     float *cur = wl;
     float4 *red = reinterpret_cast<float4 *>(wl + TP::RED);
@@ -2330,9 +2331,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
     const int64_t tile = gw;
     KArgsK *K = kargs_late();
     const int64_t P = K->a.P;
+    // pointers first: one round of kernarg loads ahead of the first wait
+    const StepPtrs b = load_ptrs(K);
     if (tile >= K->a.ntiles) return;
     STAMP(0);
-    const StepPtrs b = load_ptrs(K);
     float *wl = lds + wib * SP::FLOATS;
     float *st = wl + SP::ST;
     const int64_t e0 = tile * EPW;
@@ -2801,9 +2803,10 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
     const int64_t gw = blk * A + w;  // stamps slot
     KArgsK *K = kargs_late();
     const int64_t P = K->a.P;
-    if (blk >= K->a.ntiles) return;
-    STAMP(0);
+    // launch_block's grid is exactly ntiles blocks: no exit test, so the
+    // pointer loads below go out in the same round of kernarg loads as P
     const StepPtrs b = load_ptrs(K);
+    STAMP(0);
     float *st = lds + BP::ST;
     const int64_t e0 = blk * E;
     const int ne = (int)((P - e0) < E ? (P - e0) : E);
