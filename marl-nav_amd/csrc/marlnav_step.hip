@@ -1463,9 +1463,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
     const int64_t tile = gw;
     KArgsK *K = kargs_late();
     const int64_t P = K->a.P;
-    // pointers first: one round of kernarg loads ahead of the first wait
+    // pointers first, pinned in SGPRs before the exit test: one round of
+    // kernarg loads ahead of the first wait (the compiler would otherwise
+    // sink them below the branch, a second serial round)
     const StepPtrs b = load_ptrs(K);
-    if (tile >= K->a.ntiles) return;
+    const int64_t ntiles = K->a.ntiles;
+    asm volatile("" ::"s"(b.states), "s"(b.obstacles), "s"(b.target), "s"(b.actions),
+                 "s"(b.obs), "s"(ntiles), "s"(P));
+    if (tile >= ntiles) return;
     STAMP(0);
     float *wl = lds + wib * TP::FLOATS;
     float *cur = wl;
@@ -2331,9 +2336,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
     const int64_t tile = gw;
     KArgsK *K = kargs_late();
     const int64_t P = K->a.P;
-    // pointers first: one round of kernarg loads ahead of the first wait
+    // pointers first, pinned in SGPRs before the exit test: one round of
+    // kernarg loads ahead of the first wait (the compiler would otherwise
+    // sink them below the branch, a second serial round)
     const StepPtrs b = load_ptrs(K);
-    if (tile >= K->a.ntiles) return;
+    const int64_t ntiles = K->a.ntiles;
+    asm volatile("" ::"s"(b.states), "s"(b.obstacles), "s"(b.target), "s"(b.actions),
+                 "s"(b.obs), "s"(ntiles), "s"(P));
+    if (tile >= ntiles) return;
     STAMP(0);
     float *wl = lds + wib * SP::FLOATS;
     float *st = wl + SP::ST;
