@@ -2774,6 +2774,33 @@ __device__ __forceinline__ void block_store(float *__restrict__ dst, const float
     for (int i = (n4 << 2) + tid; i < n; i += nt) out_st<kNtRows>(dst + i, src[i]);
 }
 
+// block_store of two full spans with compile-time sizes (16-byte aligned,
+// multiples of 4 floats): every LDS read of both spans issued before the
+// first global store, so the reads' latency is paid once, not per iteration
+template <int N1, int N2, int NT>
+__device__ __forceinline__ void block_store2(float *__restrict__ d1, const float *__restrict__ s1,
+                                             float *__restrict__ d2, const float *__restrict__ s2,
+                                             int tid)
+{
+    static_assert(N1 % 4 == 0 && N2 % 4 == 0, "whole 16-byte pieces");
+    constexpr int Q1 = N1 / 4, Q2 = N2 / 4, K1 = (Q1 + NT - 1) / NT, K2 = (Q2 + NT - 1) / NT;
+    float4 v1[K1], v2[K2];
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+        if ((k + 1) * NT <= Q1 || tid + k * NT < Q1)
+            v1[k] = reinterpret_cast<const float4 *>(s1)[tid + k * NT];
+#pragma unroll
+    for (int k = 0; k < K2; ++k)
+        if ((k + 1) * NT <= Q2 || tid + k * NT < Q2)
+            v2[k] = reinterpret_cast<const float4 *>(s2)[tid + k * NT];
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+        if ((k + 1) * NT <= Q1 || tid + k * NT < Q1) out_st4<kNtRows>(d1 + 4 * (tid + k * NT), v1[k]);
+#pragma unroll
+    for (int k = 0; k < K2; ++k)
+        if ((k + 1) * NT <= Q2 || tid + k * NT < Q2) out_st4<kNtRows>(d2 + 4 * (tid + k * NT), v2[k]);
+}
+
 #ifndef MARLNAV_BLK_EARLY  // 1: stream rows/states out before the per-env phase
 #define MARLNAV_BLK_EARLY 0
 #endif
@@ -3128,7 +3155,10 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
         }
     }
     STAMP(5);
-    if (!kBlkEarly && !OBS_ONLY) {  // ---- stream the block out
+    if (!kBlkEarly && !OBS_ONLY && full && !norm) {  // ---- stream the block out
+        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
+                                               st, tid);  // (E = 64: whole 16-byte pieces)
+    } else if (!kBlkEarly && !OBS_ONLY) {
         block_store(gobs, obs_rows, nrow * D, tid, NT);
         if (norm) {
             KArgsK *kl = kargs_late();
