@@ -1,4 +1,5 @@
 # parity suite, then graph-replay A/B of libmarlnav.so against other builds
+# (scripts/build_variant.sh makes them; LIBS lists them, CFGS the configs)
 export TMPDIR=/tmp
 L=marl-nav_amd/lib
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pt.log
