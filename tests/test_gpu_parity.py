@@ -641,3 +641,40 @@ def test_reward_term_divisions_bit_exact_for_any_parameters(pkg, geom):
         np.testing.assert_array_equal(np_(env.states), exp["states"], where)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                "terminates"))
+
+
+@pytest.mark.parametrize("P,A,O", [(4096 + 7, 3, 3), (300, 3, 3), (512, 16, 32)])
+def test_non_finite_inputs_match_oracle(pkg, P, A, O):
+    """NaN / inf actions and state entries propagate exactly as in the oracle
+    (torch.clamp passes NaN, comparisons with NaN are false): states, rewards
+    and flags equal bit for bit, NaN for NaN (block, split and LPR=8 split
+    kernels; the non-finite blocks take the IEEE pair math)."""
+    g = torch.Generator().manual_seed(P + 5)
+    env = make_env(pkg, P, A, O, episode_len=50, seed=9)
+    st = env.states.cpu().clone()
+    st[3, 0, 0] = float("nan")
+    st[9, 1, 2:4] = torch.tensor([float("inf"), 0.0])
+    st[17, 2, 4] = float("-inf")
+    env.states = st
+    dm, pr = oracle_params(env)
+    form = np_(env._formation)
+    s, o, t = st.numpy(), np_(env.obstacles).copy(), np_(env.target).copy()
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    for k in range(3):
+        acts = ((torch.rand(P, A, 2, generator=g) - 0.5) * 0.8)
+        acts[5, 0, 0] = float("nan")
+        acts[40, 1, 1] = float("inf")
+        acts[41, 0, 0] = float("-inf")
+        acts = acts.numpy()
+        exp = orc.step(dm, pr, s, o, t, sn, te, acts, formation=form, step_idx=k + 1)
+        obs, rew, term, trunc = env.step(torch.from_numpy(acts).to(DEV))
+        where = f"P{P} A{A} O{O} step {k + 1}"
+        for name, got in (("states", env.states), ("obstacles", env.obstacles),
+                          ("step_num", env._step_num), ("terminates", env._terminates),
+                          ("reward", rew), ("terminated", term), ("truncated", trunc)):
+            np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
+        got = np_(obs._packed)
+        assert np.array_equal(np.isnan(got), np.isnan(exp["obs"])), where + " NaN pattern"
+        s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
+                                            "terminates"))
