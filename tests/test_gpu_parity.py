@@ -609,18 +609,21 @@ def test_every_kernel_family_bit_exact_vs_oracle(pkg, P, A, O, expect):
     assert ran == expect, (sorted(ran), sorted(expect))
 
 
+@pytest.mark.parametrize("shape", [(20000 + 3, 3, 3), (512, 16, 32)])
 @pytest.mark.parametrize("geom", [
     dict(_init_dist=7.0, _bond_sharpness=0.05, _ideal_dist=33.3, _max_at_prop_d=3),  # fast terms
     dict(_init_dist=3.0e7, _bond_sharpness=0.01, _ideal_dist=1e-30),                   # IEEE terms
     dict(_bond_sharpness=1e6, _ideal_dist=0.0, _max_at_prop_d=1.5e-6),                 # boundaries
+    dict(_bond_sharpness=0.25, _max_at_prop_d=-4.0, _ideal_dist=-12.0),                # powers of 2
 ])
-def test_reward_term_divisions_bit_exact_for_any_parameters(pkg, geom):
+def test_reward_term_divisions_bit_exact_for_any_parameters(pkg, geom, shape):
     """The reward terms divide by parameters (environment.py:236-269); the
     kernels use the short exact division sequences only when the host finds
     every such parameter inside their guards (marlnav_step, terms_fast_params)
-    and IEEE division otherwise. Rewards stay bit-exact vs the oracle
-    (which divides with IEEE division) either way."""
-    P, A, O = 20000 + 3, 3, 3
+    and IEEE division otherwise (the block kernel; the split kernel, the
+    second shape, always divides with IEEE division). Rewards stay bit-exact
+    vs the oracle (which divides with IEEE division) either way."""
+    P, A, O = shape
     g = torch.Generator().manual_seed(77)
     env = make_env(pkg, P, A, O, episode_len=40, seed=3,
                    factors=dict(risk_factor=1.5, distance_factor=3., soft_factor=7.,
