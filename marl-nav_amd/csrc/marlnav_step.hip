@@ -6,17 +6,21 @@
 // terminal logic, the masked re-initialisation of finished envs and the
 // recomputed observations of those envs.
 //
-// Mapping. The unit of work is a wave tile: W consecutive envs
-// (W = 64 / A rounded down to a multiple of 4 where possible: 20 envs at
-// A = 3) handled by ONE wavefront, one lane per agent row, env-major, so lane
-// t owns row e0*A + t of the (P*A, .) agent arrays. Every wave works alone:
-// it stages its tile's array-of-structs inputs in a wave-private LDS slice
-// with 16-byte coalesced loads (all issued before the first wait), exchanges
-// rows through that slice with wave-scope ordering only, and streams the
-// packed observation tile back out with 16-byte stores. There is no
-// __syncthreads() and no inter-wave dependency, so the waves of a CU drift
-// apart and overlap each other's memory and VALU phases. No MFMA: nothing
-// here contracts.
+// Four kernel families, one launch per step, picked on the host
+// by shape and grid size (marlnav_step, end of file):
+//   block_kernel  - one workgroup of A waves per 64 consecutive envs, lane =
+//                   env, wave = agent (the compiled A3 shapes; the headline
+//                   path), section "env-block kernel";
+//   split_kernel  - LPR lanes per agent row, wave-private tiles (A16/O32, and
+//                   small A3 grids), section "pair-split kernel";
+//   tile_kernel   - wave tiles of 64/A envs, one lane per agent row (the
+//                   compiled shapes when a buffer misses the block kernel's
+//                   alignment);
+//   wave_kernel   - generic runtime shapes.
+// All stage their inputs in LDS with LDS-DMA, keep a lane's own row in
+// registers, assemble the packed observation rows in LDS where they stream
+// out with 16-byte stores, and re-initialise / re-observe only the envs that
+// finished. No MFMA: nothing here contracts.
 //
 // Numerics: built with -ffp-contract=off and the HIP default
 // correctly rounded fp32 division and sqrt, so every distance, dot product
