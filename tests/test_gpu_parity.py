@@ -681,3 +681,41 @@ def test_non_finite_inputs_match_oracle(pkg, P, A, O):
         assert np.array_equal(np.isnan(got), np.isnan(exp["obs"])), where + " NaN pattern"
         s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))
+
+
+@pytest.mark.parametrize("P,A,O", [(2 * 1048576 + 37, 3, 3), (131072, 3, 8)])
+def test_full_size_slices_bit_exact_vs_oracle(pkg, P, A, O):
+    """Beyond BASELINE sizes (2^21 envs per GPU, ragged): envs are
+    independent and the native re-init is keyed by the global env id, so the
+    oracle stepping a contiguous slice (env_offset = its first env) must
+    reproduce the kernel's results on that slice exactly. Slices at the
+    start, in the middle and at the ragged end; 2-step episodes so most envs
+    re-initialise."""
+    g = torch.Generator(device=DEV).manual_seed(P)
+    env = make_env(pkg, P, A, O, episode_len=2, seed=31)
+    env._sync_params()
+    pr = env._cparams
+    form = np_(env._formation)
+    n = 4096
+    starts = [0, P // 2 - 1000, P - n]
+    cur = [tuple(np_(x[s:s + n]).copy() for x in (env.states, env.obstacles, env.target))
+           + (np.zeros(n, np.float32), np.zeros(n, np.bool_)) for s in starts]
+    for k in range(3):
+        acts = (torch.rand(P, A, 2, generator=g, device=DEV) - 0.5) * 0.8
+        obs, rew, term, trunc = env.step(acts)
+        for i, s in enumerate(starts):
+            dm = orc.make_dims(n, A, O, env_offset=s)
+            st, ob, tg, sn, te = cur[i]
+            exp = orc.step(dm, pr, st, ob, tg, sn, te, np_(acts[s:s + n]), formation=form,
+                           step_idx=k + 1)
+            where = f"P{P} slice {s} step {k + 1}"
+            for name, got in (("states", env.states), ("obstacles", env.obstacles),
+                              ("target", env.target), ("step_num", env._step_num),
+                              ("terminates", env._terminates), ("reward", rew),
+                              ("terminated", term), ("truncated", trunc)):
+                np.testing.assert_array_equal(np_(got[s:s + n]), exp[name], where + " " + name)
+            fg = orc.split_obs(np_(obs._packed[s:s + n]), A, O)
+            assert_obs_close(fg, dict(zip(OBS_FIELDS, orc.split_obs(exp["obs"], A, O))),
+                             prefix="", rtol=5e-7, where=where)
+            cur[i] = tuple(exp[x] for x in ("states", "obstacles", "target", "step_num",
+                                            "terminates"))
