@@ -51,6 +51,7 @@ def cli_args(**over):
 
 
 ANGLE_FIELDS = ("target_angle", "obstacles_angles", "others_angles")
+DIST_FIELDS = ("target_distance", "obstacles_distances", "others_distances")
 
 # Tolerances (north_star: obs and rewards within 1e-5 relative). Angles get an
 # absolute floor of 2e-6 rad: acos is ill-conditioned near 0 and pi, where a
@@ -60,25 +61,69 @@ RTOL = 1e-5
 ANGLE_ATOL = 2e-6
 
 
-def assert_obs_close(actual_fields, expected, prefix="obs_", rtol=RTOL, where=""):
+def _close_mask(a, e, rtol, atol):
+    """Elementwise 'outside tolerance' for float arrays that may hold
+    non-finite values: NaN must face NaN, +-inf must equal exactly, finite
+    values are compared with |a - e| <= atol + rtol*|e| (never silently true
+    for NaN, unlike the bare comparison)."""
+    a = np.asarray(a, np.float64)
+    e = np.asarray(e, np.float64)
+    an, en = np.isnan(a), np.isnan(e)
+    ai, ei = np.isinf(a), np.isinf(e)
+    fin = ~(an | en | ai | ei)
+    bad = (an != en) | ((ai | ei) & ~(an | en) & (a != e))
+    with np.errstate(invalid="ignore"):
+        bad |= fin & (np.abs(a - e) > atol + rtol * np.abs(e))
+    return a, e, bad
+
+
+def _report(what, a, e, bad):
+    i = np.argwhere(bad)[0].tolist()
+    return (f"{what}: {int(bad.sum())} of {bad.size} outside tol; first at {i}: "
+            f"got {a[tuple(i)]!r} want {e[tuple(i)]!r}")
+
+
+def assert_obs_close(actual_fields, expected, prefix="obs_", rtol=RTOL, where="",
+                     exact_distances=False):
+    """The six Observations fields against expected ones: angles within
+    rtol + ANGLE_ATOL, distances within rtol (or bit-exact with
+    ``exact_distances``, the oracle comparisons: both sides compute
+    sqrtf(fmaf(dy,dy,dx*dx)), environment.py:271-274); NaN/inf positions must
+    match in every field."""
     for f, a in zip(OBS_FIELDS, actual_fields):
         e = expected[prefix + f] if isinstance(expected, dict) or hasattr(expected, "files") \
             else expected[f]
-        a = np.asarray(a, np.float64)
-        e = np.asarray(e, np.float64)
+        if exact_distances and f in DIST_FIELDS:
+            np.testing.assert_array_equal(np.asarray(a), np.asarray(e), f"{where} {f}")
+            continue
         atol = ANGLE_ATOL if f in ANGLE_FIELDS else 0.0
-        bad = np.abs(a - e) > atol + rtol * np.abs(e)
-        assert not bad.any(), (
-            f"{where} {f}: {bad.sum()} of {bad.size} outside tol; first at "
-            f"{np.argwhere(bad)[0].tolist()}: got {a[bad][0]!r} want {e[bad][0]!r}")
+        a, e, bad = _close_mask(a, e, rtol, atol)
+        assert not bad.any(), _report(f"{where} {f}", a, e, bad)
 
 
 def assert_vec_close(a, e, rtol=RTOL, atol=0.0, what=""):
-    a = np.asarray(a, np.float64)
-    e = np.asarray(e, np.float64)
-    bad = np.abs(a - e) > atol + rtol * np.abs(e)
-    assert not bad.any(), (f"{what}: {bad.sum()} of {bad.size} outside tol; first at "
-                           f"{np.argwhere(bad)[0].tolist()}: got {a[bad][0]!r} want {e[bad][0]!r}")
+    a, e, bad = _close_mask(a, e, rtol, atol)
+    assert not bad.any(), _report(what, a, e, bad)
+
+
+def angle_error_stats(actual_fields, expected_fields):
+    """(entries needing the absolute floor, worst relative error) over the
+    angle fields - reported by the tests so the ANGLE_ATOL floor's use is
+    visible, not just tolerated."""
+    n_floor, worst = 0, 0.0
+    for f, a, e in zip(OBS_FIELDS, actual_fields, expected_fields):
+        if f not in ANGLE_FIELDS:
+            continue
+        a = np.asarray(a, np.float64)
+        e = np.asarray(e, np.float64)
+        fin = np.isfinite(a) & np.isfinite(e)
+        d = np.abs(a - e)[fin]
+        rel = d / np.maximum(np.abs(e[fin]), 1e-300)
+        n_floor += int(((d > RTOL * np.abs(e[fin])) & (d <= ANGLE_ATOL)).sum())
+        nz = np.abs(e[fin]) > 1e-3
+        if nz.any():
+            worst = max(worst, float(rel[nz].max()))
+    return n_floor, worst
 
 
 def assert_states_close(a, e, what="states"):
@@ -87,9 +132,14 @@ def assert_states_close(a, e, what="states"):
     component that cancels to ~0 is not a relative error of that component)."""
     a = np.asarray(a, np.float64)
     e = np.asarray(e, np.float64)
+    assert np.array_equal(np.isnan(a), np.isnan(e)), f"{what}: NaN pattern differs"
     assert_vec_close(a[..., [0, 1, 4]], e[..., [0, 1, 4]], what=what + "[pos,speed]")
     mag = np.linalg.norm(e[..., 2:4], axis=-1, keepdims=True)
-    bad = np.abs(a[..., 2:4] - e[..., 2:4]) > 1e-6 * np.maximum(mag, 1e-30)
+    with np.errstate(invalid="ignore"):
+        bad = np.abs(a[..., 2:4] - e[..., 2:4]) > 1e-6 * np.maximum(mag, 1e-30)
+    bad &= np.isfinite(e[..., 2:4]) & np.isfinite(mag)
+    bad |= np.isfinite(a[..., 2:4]) != np.isfinite(e[..., 2:4])
+    bad |= np.isinf(e[..., 2:4]) & (a[..., 2:4] != e[..., 2:4])
     assert not bad.any(), f"{what}[dir]: {bad.sum()} outside 1e-6*|dir|"
 
 

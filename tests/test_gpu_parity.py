@@ -120,7 +120,7 @@ def test_step_bit_exact_vs_oracle(pkg, name):
         for f, a, e in zip(OBS_FIELDS, fg, fo):
             if "distance" in f:
                 np.testing.assert_array_equal(a, e, where + " " + f)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, exact_distances=True, where=where)
 
 
 def _trace_env(pkg, name):
@@ -211,7 +211,7 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
         got = np_(obs._packed)
         Oe = dm.num_obstacles
         fg, fo = orc.split_obs(got, A, Oe), orc.split_obs(exp["obs"], A, Oe)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, exact_distances=True, where=where)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                "terminates"))
         tot += exp["counters"]
@@ -477,7 +477,7 @@ def test_extreme_coordinates_take_the_exact_path(pkg, P, A, O):
         got = np_(obs._packed)
         np.testing.assert_array_equal(got[..., 1], exp["obs"][..., 1], where)  # distances exact
         fg, fo = orc.split_obs(got, A, O), orc.split_obs(exp["obs"], A, O)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, exact_distances=True, where=where)
         s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))
 
@@ -512,7 +512,7 @@ def test_reference_rng_fresh_candidates_bit_exact_vs_oracle(pkg, P, A, O):
                           ("truncated", trunc), ("reward", rew)):
             np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
         fg, fo_ = orc.split_obs(np_(obs._packed), A, O), orc.split_obs(exp["obs"], A, O)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, exact_distances=True, where=where)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                "terminates"))
         tot += exp["counters"].astype(np.int64)
@@ -543,7 +543,7 @@ def test_native_noisy_agents_bit_exact_vs_oracle(pkg, P, A, O):
                           ("reward", rew), ("terminated", term)):
             np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
         fg, fo_ = orc.split_obs(np_(obs._packed), A, O), orc.split_obs(exp["obs"], A, O)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, exact_distances=True, where=where)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                "terminates"))
 
@@ -594,7 +594,7 @@ def test_every_kernel_family_bit_exact_vs_oracle(pkg, P, A, O, expect):
                 fg = orc.split_obs(np_(obs._packed), A, O)
                 fo = orc.split_obs(exp["obs"], A, O)
                 assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7,
-                                 where=where)
+                                 exact_distances=True, where=where)
                 st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target",
                                                        "step_num", "terminates"))
             ran.add(got_fam)
@@ -603,7 +603,7 @@ def test_every_kernel_family_bit_exact_vs_oracle(pkg, P, A, O, expect):
             assert lib.marlnav_debug_last_family() == got_fam
             fg = orc.split_obs(np_(o2._packed), A, O)
             assert_obs_close(fg, dict(zip(OBS_FIELDS, orc.split_obs(exp["obs"], A, O))),
-                             prefix="", rtol=5e-7, where=where + " observe")
+                             prefix="", rtol=5e-7, exact_distances=True, where=where + " observe")
         finally:
             lib.marlnav_debug_force_family(prev)
     assert ran == expect, (sorted(ran), sorted(expect))
@@ -679,6 +679,9 @@ def test_non_finite_inputs_match_oracle(pkg, P, A, O):
             np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
         got = np_(obs._packed)
         assert np.array_equal(np.isnan(got), np.isnan(exp["obs"])), where + " NaN pattern"
+        fg, fo_ = orc.split_obs(got, A, O), orc.split_obs(exp["obs"], A, O)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7,
+                         exact_distances=True, where=where)
         s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))
 
@@ -716,6 +719,6 @@ def test_full_size_slices_bit_exact_vs_oracle(pkg, P, A, O):
                 np.testing.assert_array_equal(np_(got[s:s + n]), exp[name], where + " " + name)
             fg = orc.split_obs(np_(obs._packed[s:s + n]), A, O)
             assert_obs_close(fg, dict(zip(OBS_FIELDS, orc.split_obs(exp["obs"], A, O))),
-                             prefix="", rtol=5e-7, where=where)
+                             prefix="", rtol=5e-7, exact_distances=True, where=where)
             cur[i] = tuple(exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))

@@ -2,6 +2,8 @@
 recycling rule (marl-nav_amd/environment.py _OutputSet)."""
 import importlib
 
+import numpy as np
+
 import torch
 
 envmod = importlib.import_module("marl-nav_amd.environment")
@@ -54,3 +56,35 @@ def test_cli_mirrors_reference_arguments():
         assert ns[k] == v, k
     assert cli.main([]) == 2          # training stays in the reference
     assert cli.main(["-re"]) == 2     # and so does rendering
+
+
+def test_comparators_see_non_finite_values():
+    """The parity comparators must not accept NaN against a number (or the
+    other way round), nor an infinity of the other sign; NaN facing NaN and
+    equal infinities pass."""
+    import pytest as _pt
+    from conftest import OBS_FIELDS, assert_obs_close, assert_states_close, assert_vec_close
+    nan, inf = float("nan"), float("inf")
+    assert_vec_close([1.0, nan, inf, -inf], [1.0, nan, inf, -inf])
+    for got, want in (([nan], [1.0]), ([1.0], [nan]), ([inf], [-inf]), ([inf], [1e38]),
+                      ([1.0], [inf])):
+        with _pt.raises(AssertionError):
+            assert_vec_close(got, want)
+    base = {f: np.ones((2, 3, 1)) for f in OBS_FIELDS}
+    for f in OBS_FIELDS:
+        bad = [base[g].copy() for g in OBS_FIELDS]
+        bad[OBS_FIELDS.index(f)][1, 2, 0] = nan
+        with _pt.raises(AssertionError):
+            assert_obs_close(bad, base, prefix="")
+        with _pt.raises(AssertionError):
+            assert_obs_close(bad, base, prefix="", exact_distances=True)
+    st = np.ones((2, 3, 5))
+    st2 = st.copy()
+    st2[0, 1, 3] = nan
+    with _pt.raises(AssertionError):
+        assert_states_close(st2, st)
+    st3 = st.copy()
+    st3[1, 0, 2] = inf
+    with _pt.raises(AssertionError):
+        assert_states_close(st3, st)
+    assert_states_close(st3, st3.copy())
