@@ -121,6 +121,37 @@ def load_library(path=None):
     return lib
 
 
+HOST_DIR = os.path.join(_HERE, "lib")
+_host = None
+
+
+def load_host():
+    """Load the native host engine ``_marlnav_host`` (csrc/host_step.cpp)
+    built in-tree next to libmarlnav.so; raise if it is missing."""
+    global _host
+    if _host is not None:
+        return _host
+    import importlib.machinery
+    import importlib.util
+    import sysconfig
+    path = os.path.join(HOST_DIR, "_marlnav_host" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} not found: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'`")
+    loader = importlib.machinery.ExtensionFileLoader("_marlnav_host", path)
+    spec = importlib.util.spec_from_file_location("_marlnav_host", path, loader=loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    _host = mod
+    return mod
+
+
+def fn_addr(cfunc):
+    """Address of a ctypes-bound C function (for the host engine)."""
+    return ctypes.cast(cfunc, ctypes.c_void_p).value
+
+
 def check(rc, lib=None):
     if rc != 0:
         lib = lib or load_library()

@@ -13,6 +13,11 @@ Differences from the reference, all deliberate:
 * ``states``/``obstacles``/``target`` are device buffers updated in place by
   each step (the reference rebinds them to new tensors); clone to snapshot.
 * The episode counters live on the device; reading one synchronises.
+* ``env.step`` is the native host engine (``abi.load_host()``, C++): it
+  checks the actions, picks the output tensors and enqueues the kernel
+  (host side); ``Env._step_py`` handles everything the fast
+  path does not (action coercion, parameter changes, reference-RNG and mock
+  modes) and launches through the same engine.
 * Re-initialisation randomness: ``params['rng']`` selects
   ``'native'`` (default for the triangle init: a Philox4x32-10 stream keyed
   by (seed, global env id, step), drawn on the GPU only for finished envs) or
@@ -22,7 +27,7 @@ Differences from the reference, all deliberate:
 """
 import ctypes
 import math
-import sys
+import weakref
 
 import torch
 
@@ -154,21 +159,13 @@ class Env(object):
             # generator before the init sampler does (environment.py:26)
             seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self._rng == 'native' else 0
         self._seed = int(seed) & (2 ** 64 - 1)
-        self._step_idx = 0
         self._normalizer = None
         self._obs_norm_buffers = None
         self._action_scaler = None
-        self._buf_gen = 0          # bumped whenever a device buffer is replaced
-        self._out_pool = []        # reusable step outputs (_OutputSet)
-        self._out_next = 0
-        self._last_out = None
+        self._engine = None
 
         self._dims = abi.MarlnavDims()
         self._cparams = abi.MarlnavParams()
-        self._bufs = abi.MarlnavStepBuffers()
-        self._dims_ref = ctypes.byref(self._dims)
-        self._cparams_ref = ctypes.byref(self._cparams)
-        self._bufs_ref = ctypes.byref(self._bufs)
         self._formation = None
         if is_triangle:
             smp = self._init_sampler
@@ -191,20 +188,50 @@ class Env(object):
         else:
             st, ob, tg = self._init_sampler()
             self._set_state_buffers(st, ob, tg)
-        self._step_idx = 1
         self._step_num = torch.zeros(P, device=self.device)
         self._terminates = torch.zeros(P, dtype=torch.bool, device=self.device)
-        self._reinit_mask = torch.zeros(P, device=self.device)
-        self._last_finished = None
         self._counters = torch.zeros(3, self._slots(), dtype=torch.int64,
                                      device=self.device)
         self._counter_out = torch.zeros(3, dtype=torch.int64, device=self.device)
+        wr = weakref.ref(self)   # the engine must not keep the Env alive
+        eng = abi.load_host().Engine(
+            abi.fn_addr(self._lib.marlnav_step), abi.fn_addr(self._lib.marlnav_last_error),
+            torch._C._cuda_getCurrentRawStream, self.device.index,
+            lambda: _new_output_set(wr()), lambda a: wr()._step_py(a))
+        object.__setattr__(self, '_engine', eng)
+        object.__setattr__(self, 'step', eng)   # Env.step: the engine's fast path
+        self._reinit_mask = torch.zeros(P, device=self.device)
+        self._configure()
 
     # ------------------------------------------------------------ plumbing
     def __setattr__(self, name, value):
-        if name in _PARAM_ATTRS:
+        if name in _PARAM_ATTRS or name == '_init_sampler':
             object.__setattr__(self, '_params_dirty', True)
+            eng = self.__dict__.get('_engine')
+            if eng is not None:
+                eng.fast_ok = 0   # next step goes through _step_py
         object.__setattr__(self, name, value)
+
+    def _configure(self):
+        """Push dims, parameters and the current device buffers to the host
+        engine (after any of them changed)."""
+        eng = self.__dict__.get('_engine')
+        if eng is None:
+            return
+        b = abi.MarlnavStepBuffers()
+        b.states = self._states.data_ptr()
+        b.obstacles = self._obstacles.data_ptr()
+        b.target = self._target.data_ptr()
+        b.step_num = self.__dict__['_step_num_t'].data_ptr()
+        b.terminates = self.__dict__['_terminates_t'].data_ptr()
+        b.counters = self._counters.data_ptr()
+        b.formation = self._formation.data_ptr() if self._formation is not None else None
+        if self._obs_norm_buffers is not None:
+            b.norm_mean = self._obs_norm_buffers[0].data_ptr()
+            b.norm_scale = self._obs_norm_buffers[1].data_ptr()
+        fast = (not self._params_dirty and self._rng == 'native'
+                and self._init_sampler is self._default_init_sampler)
+        eng.configure(bytes(self._dims), bytes(self._cparams), bytes(b), fast)
 
     def _slots(self):
         n = self._lib.marlnav_counter_slots(ctypes.byref(self._dims))
@@ -240,7 +267,7 @@ class Env(object):
         if target is not None:
             object.__setattr__(self, '_target', own(target, (P, 1, 2)))
         self._update_dims()
-        self.__dict__['_buf_gen'] = self.__dict__.get('_buf_gen', 0) + 1
+        self._configure()
 
     def _update_dims(self):
         S = int(self._obstacles.shape[1])
@@ -257,7 +284,9 @@ class Env(object):
         self._act_shape = (self.num_parallel, self.num_agents, 2)
         O = d.num_obstacles
         self._split = [1, 1, O, O, self.num_agents - 1, self.num_agents - 1]
-        self.__dict__['_out_pool'] = []  # output shapes may have changed
+        eng = self.__dict__.get('_engine')
+        if eng is not None:
+            eng.reset_pool()               # output shapes may have changed
         if hasattr(self, '_counters') and old != (d.num_agents, d.num_obstacles, S):
             totals = self._counter_totals()
             self._counters = torch.zeros(3, self._slots(), dtype=torch.int64,
@@ -276,8 +305,8 @@ class Env(object):
             self._cparams.act_scale[:] = [float(x) for x in sc.scale.float().reshape(-1)]
             self._cparams.act_mean[:] = [float(x) for x in sc.mean.float().reshape(-1)]
             self._cparams.flags |= abi.SCALE_ACTIONS
-        self._cparams_ref = ctypes.byref(self._cparams)
         object.__setattr__(self, '_params_dirty', False)
+        self._configure()
 
     def _new_obs(self):
         return torch.empty(self.num_parallel, self.num_agents, self._obs_dim,
@@ -322,7 +351,7 @@ class Env(object):
     @_step_num.setter
     def _step_num(self, value):
         self.__dict__['_step_num_t'] = self._dev_f32(value, (self.num_parallel,))
-        self.__dict__['_buf_gen'] = self.__dict__.get('_buf_gen', 0) + 1
+        self._configure()
 
     @property
     def _terminates(self):
@@ -334,20 +363,26 @@ class Env(object):
         if tuple(t.shape) != (self.num_parallel,):
             raise ValueError(f"_terminates must be ({self.num_parallel},)")
         self.__dict__['_terminates_t'] = t
-        self.__dict__['_buf_gen'] = self.__dict__.get('_buf_gen', 0) + 1
+        self._configure()
 
     @property
     def _reinit_mask(self):
-        m = self.__dict__.get('_reinit_mask_t')
-        if m is None and self._last_finished is not None:
-            term, trunc = self._last_finished
-            m = torch.where(torch.logical_or(trunc, term), 1, 0)  # environment.py:102-103
-            self.__dict__['_reinit_mask_t'] = m
-        return m
+        """environment.py:102-103: set by reset(), overwritten by every step
+        with where(truncated | terminated, 1, 0) (int64)."""
+        eng = self._engine
+        if eng.steps_done != self.__dict__.get('_reinit_mask_at'):
+            last = eng.last_finished()
+            if last is not None:
+                term, trunc = last
+                self.__dict__['_reinit_mask_t'] = torch.where(torch.logical_or(trunc, term), 1, 0)
+                self.__dict__['_reinit_mask_at'] = eng.steps_done
+        return self.__dict__.get('_reinit_mask_t')
 
     @_reinit_mask.setter
     def _reinit_mask(self, value):
         self.__dict__['_reinit_mask_t'] = value
+        eng = self.__dict__.get('_engine')
+        self.__dict__['_reinit_mask_at'] = eng.steps_done if eng is not None else None
 
     # episode statistics (environment.py:43-45); MAPPO reads and zeroes them
     def _counter_totals(self):
@@ -389,10 +424,10 @@ class Env(object):
         """Have every step also write ``normalizer``'s output (utils.py:519-532)
         from the kernel; ``normalizer(obs)`` then returns it without work."""
         self._normalizer = normalizer
-        self._out_pool = []
-        self._buf_gen += 1
+        self._engine.reset_pool()
         if normalizer is None:
             self._obs_norm_buffers = None
+            self._configure()
             return
         D = self._obs_dim
         mean = normalizer.mean.to(self.device, _F32).reshape(-1).contiguous()
@@ -400,6 +435,7 @@ class Env(object):
         if mean.numel() != D or scale.numel() != D:
             raise ValueError(f"normalizer has {mean.numel()} features, env rows have {D}")
         self._obs_norm_buffers = (mean, scale)
+        self._configure()
 
     def attach_action_scaler(self, scaler):
         """Have every step read raw policy actions in [-1, 1] and apply
@@ -410,6 +446,7 @@ class Env(object):
             raise ValueError("ActionScaler must have 2 action components (angle, accel)")
         self._action_scaler = scaler
         object.__setattr__(self, '_params_dirty', True)
+        self._engine.fast_ok = 0
 
     def reset(self):
         """environment.py:70-74: marks every env for re-init and returns the
@@ -439,166 +476,78 @@ class Env(object):
             raise ValueError(f"actions must be {self._act_shape}, got {tuple(actions.shape)}")
         return actions
 
-    def _take_outputs(self):
-        """This step's output set: a pooled one nothing references any more,
-        else a new allocation (pooled while the pool is small)."""
-        pool = self._out_pool
-        capturing = torch.cuda.is_current_stream_capturing()
-        if pool and not capturing:
-            last = self._last_out
-            n = len(pool)
-            i = self._out_next
-            for _ in range(2 if n > 1 else 1):
-                out = pool[i]
-                i = i + 1 if i + 1 < n else 0
-                if out is not last and out.free():
-                    self._out_next = i
-                    return out
-        out = _OutputSet(self)
-        if not capturing and len(pool) < _POOL_MAX:
-            pool.append(out)
-            out.arm()
-        return out
-
-    def _fill_buffers(self, b):
-        """Point a step-buffer struct at the env's current device buffers."""
-        b.states = self._states.data_ptr()
-        b.obstacles = self._obstacles.data_ptr()
-        b.target = self._target.data_ptr()
-        b.step_num = self.__dict__['_step_num_t'].data_ptr()
-        b.terminates = self.__dict__['_terminates_t'].data_ptr()
-        b.counters = self._counters.data_ptr()
-        b.formation = self._formation.data_ptr() if self._formation is not None else None
-        if self._obs_norm_buffers is not None:
-            b.norm_mean = self._obs_norm_buffers[0].data_ptr()
-            b.norm_scale = self._obs_norm_buffers[1].data_ptr()
-
     def step(self, actions):
         """environment.py:92-107: returns (Observations, rewards (P,),
         terminated (P,) bool, truncated (P,) bool). The returned tensors are
         never aliased with any tensor still referenced from a previous step;
-        their memory is recycled only once nothing refers to it."""
+        their memory is recycled only once nothing refers to it.
+
+        (An Env instance's ``step`` attribute is the native host engine; this
+        method is what it runs for calls its fast path does not take.)"""
+        return self._engine(actions)
+
+    @property
+    def _step_idx(self):
+        return self._engine.step_idx
+
+    def _step_py(self, actions):
+        """The step for everything the engine's fast path does not take:
+        pending parameter changes, actions that need coercion (dtype, device,
+        strides, a wider last axis), the reference-RNG / mock-initializer
+        modes (the host init sampler is called every step, environment.py:78)."""
         if self._params_dirty:
             self._sync_params()
         dev = self.device
         if not (type(actions) is torch.Tensor and actions.dtype is _F32
                 and actions.device == dev and actions.shape == self._act_shape
-                and actions.is_contiguous()):
+                and actions.is_contiguous() and not actions.requires_grad):
             actions = self._coerce_actions(actions)
-        d = self.__dict__
-        out = self._take_outputs()
-        b = out.bufs
-        if out.gen != d['_buf_gen']:
-            self._fill_buffers(b)
-            out.gen = d['_buf_gen']
-        b.actions = actions.data_ptr()
-        cp = self._cparams
-        flags = cp.flags & ~(abi.FRESH_STATES_FROM_MOVED | abi.WRITE_OBS_NORM)
-        keep = None
+        eng = self._engine
         if self._rng == 'native' and self._init_sampler is self._default_init_sampler:
-            if out.fresh:
-                b.fresh_states = b.fresh_obstacles = b.fresh_target = None
-                out.fresh = False
-        else:
-            P = self.num_parallel
-            fs, fo, ft = self._init_sampler()                # environment.py:78
-            S = self._obstacles.shape[1]
-            keep = (self._dev_f32(fs, (P, self.num_agents, 5)),
-                    self._dev_f32(fo, (P, S, 2)), self._dev_f32(ft, (P, 1, 2)))
-            b.fresh_states, b.fresh_obstacles, b.fresh_target = (t.data_ptr() for t in keep)
-            out.fresh = True
-            if self._mock_alias:
-                flags |= abi.FRESH_STATES_FROM_MOVED
-        if out.normalized is not None:
-            flags |= abi.WRITE_OBS_NORM
-        cp.flags = flags
-        rc = self._lib.marlnav_step(self._dims_ref, self._cparams_ref, out.bufs_ref,
-                                    d['_step_idx'], _stream_handle(dev))
-        if rc:
-            abi.check(rc, self._lib)
-        d['_step_idx'] += 1
+            if not eng.fast_ok:
+                self._configure()
+            return eng.launch(actions.data_ptr(), None, 0)
+        P = self.num_parallel
+        fs, fo, ft = self._init_sampler()                # environment.py:78
+        S = self._obstacles.shape[1]
+        keep = (self._dev_f32(fs, (P, self.num_agents, 5)),
+                self._dev_f32(fo, (P, S, 2)), self._dev_f32(ft, (P, 1, 2)))
+        flags = abi.FRESH_STATES_FROM_MOVED if self._mock_alias else 0
+        out = eng.launch(actions.data_ptr(), tuple(t.data_ptr() for t in keep), flags)
         if self._mock_alias:
             # the reference's MockInitializer now holds the post-move states
             # (utils.py:310-319 aliasing); later re-inits restore them
-            d['_mock_alias'] = False
+            self._mock_alias = False
             init = self._init_sampler
             if isinstance(init, MockInitializer):
                 init.states = self._states.clone()
-        d['_last_out'] = out
-        d['_last_finished'] = (out.terminated, out.truncated)
-        d['_reinit_mask_t'] = None
-        del keep
-        return out.obs, out.reward, out.terminated, out.truncated
+        del keep   # stream-ordered: the caching allocator reuses them after the kernel
+        return out
 
 
-_POOL_MAX = 4
+def _new_output_set(env):
+    """One step's output tensors carved from ONE device allocation: packed
+    observations (and the fused normaliser's copy), reward, terminated,
+    truncated; returns (Observations, reward, terminated, truncated, packed,
+    normalized-or-None) for the host engine's pool."""
+    P, A, D = env._obs_shape
+    nobs = P * A * D * 4
+    norm = env._obs_norm_buffers is not None
 
-
-class _OutputSet(object):
-    """The output tensors of one step carved from ONE device allocation:
-    packed observations (and the fused-normalizer copy), reward, terminated,
-    truncated, plus the Observations tuple of views and a step-buffer struct
-    pointing at them. A pooled set is handed out again only when nothing
-    outside the env refers to it: no extra Python reference to any object
-    it handed out and no other tensor viewing its storage (so a caller that
-    keeps any output, or a view of one, never sees it overwritten)."""
-    __slots__ = ('obs', 'packed', 'normalized', 'reward', 'terminated', 'truncated',
-                 'bufs', 'bufs_ref', 'gen', 'fresh', '_cdata', '_objs', '_base_use',
-                 '_base_refs')
-
-    def __init__(self, env):
-        P, A, D = env._obs_shape
-        dev = env.device
-        nobs = P * A * D * 4
-        norm = env._obs_norm_buffers is not None
-
-        def up(n):
-            return (n + 255) & ~255
-        o_norm = up(nobs)
-        o_rew = o_norm + (up(nobs) if norm else 0)
-        o_term = o_rew + up(4 * P)
-        o_trunc = o_term + up(P)
-        buf = torch.empty(o_trunc + up(P), dtype=torch.uint8, device=dev)
-        self.packed = buf[:nobs].view(_F32).view(P, A, D)
-        self.normalized = buf[o_norm:o_norm + nobs].view(_F32).view(P, A, D) if norm else None
-        self.reward = buf[o_rew:o_rew + 4 * P].view(_F32)
-        self.terminated = buf[o_term:o_term + P].view(torch.bool)
-        self.truncated = buf[o_trunc:o_trunc + P].view(torch.bool)
-        self.obs = env._wrap_obs(self.packed, self.normalized)
-        self._cdata = buf.untyped_storage()._cdata
-        del buf
-        self.bufs = abi.MarlnavStepBuffers()
-        self.bufs_ref = ctypes.byref(self.bufs)
-        b = self.bufs
-        b.obs = self.packed.data_ptr()
-        b.reward = self.reward.data_ptr()
-        b.terminated = self.terminated.data_ptr()
-        b.truncated = self.truncated.data_ptr()
-        if norm:
-            b.obs_norm = self.normalized.data_ptr()
-        self.gen = -1
-        self.fresh = True
-        self._objs = None
-
-    def arm(self):
-        """Record the reference counts that mean 'held by the pool only'."""
-        objs = (self.obs, self.packed, self.reward, self.terminated,
-                self.truncated) + tuple(self.obs)
-        if self.normalized is not None:
-            objs = objs + (self.normalized,)
-        self._objs = objs
-        self._base_use = torch._C._storage_Use_Count(self._cdata)
-        self._base_refs = _refcounts(objs)
-
-    def free(self):
-        return (torch._C._storage_Use_Count(self._cdata) == self._base_use
-                and _refcounts(self._objs) == self._base_refs)
-
-
-def _refcounts(objs):
-    # one code path for the baseline and the check: the counts include this
-    # function's own temporary references identically
-    return [sys.getrefcount(x) for x in objs]
+    def up(n):
+        return (n + 255) & ~255
+    o_norm = up(nobs)
+    o_rew = o_norm + (up(nobs) if norm else 0)
+    o_term = o_rew + up(4 * P)
+    o_trunc = o_term + up(P)
+    buf = torch.empty(o_trunc + up(P), dtype=torch.uint8, device=env.device)
+    packed = buf[:nobs].view(_F32).view(P, A, D)
+    normalized = buf[o_norm:o_norm + nobs].view(_F32).view(P, A, D) if norm else None
+    reward = buf[o_rew:o_rew + 4 * P].view(_F32)
+    terminated = buf[o_term:o_term + P].view(torch.bool)
+    truncated = buf[o_trunc:o_trunc + P].view(torch.bool)
+    obs = env._wrap_obs(packed, normalized)
+    return obs, reward, terminated, truncated, packed, normalized
 
 
 class _PackedObservations(Observations):

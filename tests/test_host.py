@@ -10,7 +10,7 @@ envmod = importlib.import_module("marl-nav_amd.environment")
 
 
 class _Stub:
-    """The attributes _OutputSet reads from an Env."""
+    """The attributes _new_output_set reads from an Env."""
     _obs_shape = (10, 3, 12)
     device = torch.device("cpu")
     _obs_norm_buffers = None
@@ -20,29 +20,87 @@ class _Stub:
 
 
 def test_output_set_layout():
-    s = envmod._OutputSet(_Stub())
-    assert s.packed.shape == (10, 3, 12) and s.packed.dtype == torch.float32
-    assert s.reward.shape == (10,) and s.terminated.dtype == torch.bool
-    assert [tuple(f.shape) for f in s.obs] == [(10, 3, 1), (10, 3, 1), (10, 3, 3), (10, 3, 3),
-                                               (10, 3, 2), (10, 3, 2)]
+    obs, reward, term, trunc, packed, norm = envmod._new_output_set(_Stub())
+    assert norm is None
+    assert packed.shape == (10, 3, 12) and packed.dtype == torch.float32
+    assert reward.shape == (10,) and term.dtype == torch.bool
+    assert [tuple(f.shape) for f in obs] == [(10, 3, 1), (10, 3, 1), (10, 3, 3), (10, 3, 3),
+                                             (10, 3, 2), (10, 3, 2)]
     # one allocation, disjoint regions
     regions = sorted((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size())
-                     for t in (s.packed, s.reward, s.terminated, s.truncated))
+                     for t in (packed, reward, term, trunc))
     assert all(a[1] <= b[0] for a, b in zip(regions, regions[1:]))
-    assert s.obs._packed is s.packed
+    assert obs._packed is packed
 
 
-def test_output_set_is_free_only_when_unreferenced():
-    s = envmod._OutputSet(_Stub())
-    s.arm()
-    assert s.free()
-    held = [lambda: s.reward, lambda: s.obs, lambda: s.obs[3], lambda: s.obs.target_angle[2:4],
-            lambda: s.packed.view(-1), lambda: s.truncated[1:], lambda: (s.obs, s.reward)]
-    for make in held:
-        x = make()
-        assert not s.free()
-        del x
-        assert s.free()
+def _cpu_engine(calls):
+    """The native host engine with a stand-in step function (records the
+    output pointers it is given, returns 0) and CPU tensors: exercises the
+    output-set pool without a GPU."""
+    import ctypes
+    abi = importlib.import_module("marl-nav_amd.abi")
+    host = abi.load_host()
+    proto = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.POINTER(abi.MarlnavStepBuffers), ctypes.c_uint64,
+                             ctypes.c_void_p)
+
+    def fake_step(d, p, b, idx, stream):
+        calls.append((b.contents.obs, idx))
+        return 0
+    cb = proto(fake_step)
+    stub = _Stub()
+    eng = host.Engine(abi.fn_addr(cb), 0, lambda i: 0, -1,
+                      lambda: envmod._new_output_set(stub), lambda a: None)
+    dims = abi.MarlnavDims(num_parallel=10, num_agents=3, num_obstacles=3, obstacle_stride=3)
+    eng.configure(bytes(dims), bytes(abi.MarlnavParams()), bytes(abi.MarlnavStepBuffers()), True)
+    return eng, cb
+
+
+def test_engine_recycles_an_output_set_only_when_unreferenced():
+    calls = []
+    eng, cb = _cpu_engine(calls)
+    first = eng.launch(0, None, 0)
+    obs, rew, term, trunc = first
+    ptr0 = calls[-1][0]
+    del first, obs, rew, term, trunc
+    # nothing held: after another step the first set is reused (never the
+    # set of the previous step)
+    eng.launch(0, None, 0)
+    eng.launch(0, None, 0)
+    assert calls[-1][0] == ptr0
+    assert [c[1] for c in calls] == [1, 2, 3]      # step index advances per launch
+    # any kept object or view keeps its set out of the pool's reuse
+    for k in range(8):
+        out = eng.launch(0, None, 0)
+        keep = [lambda o: o[1], lambda o: o[0], lambda o: o[0][3], lambda o: o[0].target_angle[2:4],
+                lambda o: o[0]._packed.view(-1), lambda o: o[3][1:], lambda o: o[2],
+                lambda o: o[0]._packed][k](out)
+        kept_ptr = calls[-1][0]
+        del out
+        for _ in range(6):
+            eng.launch(0, None, 0)
+            assert calls[-1][0] != kept_ptr, k
+        del keep
+    assert len(eng.pool_info()) <= 4
+
+
+def test_engine_fast_path_falls_back_for_other_actions():
+    calls = []
+    _, cb = _cpu_engine(calls)
+    seen = []
+    abi = importlib.import_module("marl-nav_amd.abi")
+    host = abi.load_host()
+    stub = _Stub()
+    eng = host.Engine(abi.fn_addr(cb), 0, lambda i: 0, 0,
+                      lambda: envmod._new_output_set(stub), lambda a: seen.append(a) or "slow")
+    dims = abi.MarlnavDims(num_parallel=10, num_agents=3, num_obstacles=3, obstacle_stride=3)
+    eng.configure(bytes(dims), bytes(abi.MarlnavParams()), bytes(abi.MarlnavStepBuffers()), True)
+    # CPU tensors are never taken by the fast path (it wants the env's HIP device)
+    assert eng(torch.zeros(10, 3, 2)) == "slow" and len(seen) == 1
+    assert eng([1, 2]) == "slow"
+    eng.fast_ok = 0
+    assert eng(torch.zeros(10, 3, 2)) == "slow"
+    assert calls == []
 
 
 def test_cli_mirrors_reference_arguments():
