@@ -1,8 +1,10 @@
 """Benchmark: env-steps/s of the drop-in Env.step on MI355X.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
-the driver launches one rank per GPU with torch.distributed.run. Rank 0
-prints ONE JSON line.
+the driver launches one rank per GPU with torch.distributed.run. Run as a
+plain process with ``--gpus N`` > 1, bench.py starts that launcher itself
+(before touching the GPU) and exits with its status. Rank 0 prints ONE JSON
+line.
 
 Workload (BASELINE.json configs[2]): per GPU 65,536 envs x
 3 agents x 3 obstacles, fp32, default reward factors, episode_len 200, native
@@ -15,31 +17,40 @@ Python API, returning fresh observation/reward/done tensors.
 Timing: W untimed steps; barrier + synchronize; K timed steps; synchronize +
 barrier; the max over ranks. value = N*P*K / max time.
 
-roofline: the step kernel's average duration from HIP events recorded on the
-launch stream (torch's current stream, where Env.step enqueues) around the
-timed region, divided by K (an upper bound: inter-kernel gaps are included),
-against the algorithmic bytes per env-step (read 28A+8O+13, write
-20A+4A*D+11: 336 B at A3/O3) and the 8 TB/s HBM peak. kernel_us_graph: the
-same from replays of a hipGraph of back-to-back Env.step launches, for
-reference. traffic: HBM bytes per launch from the committed rocprofv3 PMC
-summary for this config (profiles/), or null.
+roofline (the step kernel): ``kernel_us`` = average duration of one step
+launch, from HIP events on the launch stream around replays of a hipGraph of
+back-to-back Env.step launches (of a second Env of the same shape, so the
+timed env's state and counters are untouched); ``achieved`` = algorithmic
+bytes per launch (read 28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at
+A3/O3) / ``kernel_us``, against the 8 TB/s HBM peak. ``timed_region_us`` =
+HIP events on the same stream around the K timed steps, per step (includes
+any gap the host leaves between launches). ``traffic``: HBM bytes per launch
+from the committed rocprofv3 PMC summary for this config (profiles/; not
+measured in this run - the source is named), or null.
 
 cpu_baseline (rank 0, N=1): oracle/torch_ref.py - the reference's step
-restated with its own execution structure in eager PyTorch on the host CPU -
-timed on a bounded sample of the same workload.
+restated with its own execution structure in eager PyTorch (pinned bit for
+bit to the reference's golden vectors, tests/test_torch_ref.py) - timed on
+the host CPU with all available cores and with one thread on a bounded
+sample of the same workload; plus the same restatement run eagerly on the
+GPU (how the reference itself runs there).
 """
 import argparse
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 
 HBM_PEAK_GBS = 8000.0
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
 def alg_bytes_per_env(A, O):
@@ -47,7 +58,7 @@ def alg_bytes_per_env(A, O):
     return (28 * A + 8 * O + 13) + (20 * A + 4 * A * D + 11)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
@@ -56,17 +67,29 @@ def parse():
     ap.add_argument("--agents", type=int, default=3)
     ap.add_argument("--obstacles", type=int, default=3)
     ap.add_argument("--cpu-baseline", choices=("auto", "on", "off"), default="auto")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
-    return ap.parse_args()
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="seconds of CPU-baseline work per thread setting")
+    ap.add_argument("--pmc", default=PMC_SUMMARY)
+    return ap.parse_args(argv)
 
 
-def make_env(pkg, P, A, O, device, rank):
+def self_launch(a):
+    """--gpus N > 1 outside torch.distributed.run: start the launcher as a
+    child (this process has not touched the GPU) and return its status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def make_env(pkg, P, A, O, device, rank, seed=20251003):
     args = pkg.default_args(num_parallel=P, num_agents=A, num_obstacles=O)
     params = pkg.set_env_params(args, device)
     params["rng"] = "native"
-    params["seed"] = 20251003
+    params["seed"] = seed
     params["env_offset"], _ = pkg.shard.weak_slice(rank, P)
     return pkg.Env(params)
 
@@ -83,10 +106,10 @@ def make_actions(P, A, device, rank, n=64):
 
 
 def kernel_time_us(env, actions, n=25, replays=12):
-    """Average step-kernel time from HIP events on the launch stream around
-    replays of a hipGraph holding n back-to-back Env.step launches (no host
-    gaps between kernels; each interval includes the graph's inter-kernel
-    boundary, so this slightly overstates the kernel duration)."""
+    """Average step-launch duration: HIP events on the launch stream around
+    replays of a hipGraph holding n back-to-back Env.step launches of ``env``
+    (each interval includes the graph's inter-kernel boundary, as a
+    back-to-back rocprofv3 kernel duration does). Returns (mean, median)."""
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -113,28 +136,81 @@ def kernel_time_us(env, actions, n=25, replays=12):
     return sum(per) / len(per), per[len(per) // 2]
 
 
-def cpu_baseline(P, A, O, seconds, threads):
+def host_cpu_facts():
+    model = platform.processor() or "?"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "os_cpu_count": os.cpu_count(),
+            "sched_getaffinity": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def time_torch_ref(P, A, O, seconds, threads=None, device="cpu"):
+    """Steps/s of oracle/torch_ref.py over a bounded sample; returns
+    (env-steps/s, steps, seconds)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from torch_ref import TorchRefEnv
     prev = torch.get_num_threads()
-    torch.set_num_threads(threads)
+    if threads:
+        torch.set_num_threads(threads)
     try:
-        env = TorchRefEnv(P, A, O, seed=7)
+        env = TorchRefEnv(P, A, O, seed=7, device=device)
         g = torch.Generator().manual_seed(99)
         acts = [torch.stack([torch.rand(P, A, generator=g) - 0.5,
-                             torch.rand(P, A, generator=g) - 0.5], 2) for _ in range(4)]
+                             torch.rand(P, A, generator=g) - 0.5], 2).to(device)
+                for _ in range(4)]
         env.step(acts[0])
+        if device != "cpu":
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         n = 0
         while True:
             env.step(acts[n % 4])
             n += 1
-            if time.perf_counter() - t0 > seconds or n >= 1000:
+            if time.perf_counter() - t0 > seconds or n >= 2000:
                 break
+        if device != "cpu":
+            torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     finally:
         torch.set_num_threads(prev)
     return P * n / dt, n, dt
+
+
+def cpu_baseline(P, A, O, seconds, device):
+    facts = host_cpu_facts()
+    # all cores the process may run on (the cgroup quota caps how many of
+    # them it gets; more threads than that only oversubscribe)
+    n_all = facts["sched_getaffinity"]
+    if facts["cgroup_cpu_quota"]:
+        n_all = max(1, min(n_all, int(facts["cgroup_cpu_quota"])))
+    v_all, n1, s1 = time_torch_ref(P, A, O, seconds, threads=n_all)
+    v_one, n2, s2 = time_torch_ref(P, A, O, seconds, threads=1)
+    v_gpu, n3, s3 = time_torch_ref(P, A, O, seconds / 2, device=str(device))
+    return {"value": v_all, "unit": "env-steps/s", "cores": n_all, "kind": "port",
+            "value_1thread": v_one,
+            "sample": (f"oracle/torch_ref.py (the reference's step structure, eager torch; "
+                       f"bit-exact vs the reference goldens): {P} envs x {A} agents x {O} "
+                       f"obstacles, {n1} steps in {s1:.1f} s on {n_all} threads, {n2} steps "
+                       f"in {s2:.1f} s on 1 thread, after 1 warm-up step"),
+            "host": facts,
+            "secondary_eager_torch_gpu": {"value": v_gpu, "unit": "env-steps/s",
+                                          "sample": f"same restatement on {device}: {n3} "
+                                                    f"steps in {s3:.1f} s"}}
 
 
 def load_traffic(path, workload):
@@ -142,21 +218,22 @@ def load_traffic(path, workload):
         with open(path) as fh:
             pmc = json.load(fh)
     except (OSError, ValueError):
-        return None
+        return None, None
     ent = pmc.get(workload)
     if not ent:
-        return None
-    return ent.get("hbm_bytes_per_launch")
+        return None, None
+    return ent.get("hbm_bytes_per_launch"), ent.get("source", os.path.relpath(path, ROOT))
 
 
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and a.gpus > 1 and "LOCAL_RANK" not in os.environ:
+        return self_launch(a)
+    if world != a.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {a.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world > 1:
-            raise SystemExit(f"WORLD_SIZE={world} but --gpus {a.gpus}")
     # MARLNAV_BENCH_BACKEND=gloo rehearses the N>1 path on fewer GPUs than
     # ranks (ranks share devices; reductions on the host)
     backend = os.environ.get("MARLNAV_BENCH_BACKEND", "nccl")
@@ -176,6 +253,11 @@ def main():
     P, A, O = a.envs, a.agents, a.obstacles
     env = make_env(pkg, P, A, O, device, rank)
     actions = make_actions(P, A, device, rank)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record()   # the first timing event of a process is slow to record:
+    ev1.record()   # pay that here, outside the timed region
+    ev1.synchronize()
 
     for i in range(a.warmup):
         env.step(actions[i % len(actions)])
@@ -186,8 +268,6 @@ def main():
 
     barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
     for i in range(a.steps):
@@ -197,28 +277,24 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     dt = pkg.shard.max_over_ranks(dt, red_dev)
-    kern_avg = ev0.elapsed_time(ev1) * 1e3 / a.steps  # us per step-kernel, timed region
+    region_us = ev0.elapsed_time(ev1) * 1e3 / a.steps
+    counters = pkg.shard.sum_over_ranks([env._num_trunc, env._num_col, env._num_tar], red_dev)
 
-    kern_graph, kern_med = kernel_time_us(env, actions)
+    kenv = make_env(pkg, P, A, O, device, rank, seed=20251004)
+    kern_us, kern_med = kernel_time_us(kenv, actions)
+    del kenv
     per_env = alg_bytes_per_env(A, O)
     launch_bytes = per_env * P
-    achieved = launch_bytes / (kern_avg * 1e-6) / 1e9
-    workload = f"P{P}_A{A}_O{O}"
-    traffic = load_traffic(a.pmc, workload)
+    achieved = launch_bytes / (kern_us * 1e-6) / 1e9
+    traffic, traffic_src = load_traffic(a.pmc, f"P{P}_A{A}_O{O}")
 
     cpu = None
     want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and world == 1)
     if rank == 0 and want_cpu:
-        threads = a.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        v, n, secs = cpu_baseline(P, A, O, a.cpu_seconds, threads)
-        cpu = {"value": v, "unit": "env-steps/s", "cores": threads, "kind": "port",
-               "sample": (f"oracle/torch_ref.py (reference step structure, eager torch "
-                          f"CPU): {n} steps x {P} envs x {A} agents x {O} obstacles "
-                          f"in {secs:.1f} s after 1 warm-up step; host os.cpu_count()="
-                          f"{os.cpu_count()}")}
+        cpu = cpu_baseline(P, A, O, a.cpu_seconds, device)
 
-    counters = pkg.shard.sum_over_ranks([env._num_trunc, env._num_col, env._num_tar], red_dev)
     if rank == 0:
+        cfg_name = "BASELINE configs[2]" if (P, A, O) == (65536, 3, 3) else "custom"
         line = {
             "metric": "env-steps/sec (whole node) at 3 agents; 1/2/4/8-GPU scaling + %HBM roofline",
             "value": world * P * a.steps / dt,
@@ -233,15 +309,15 @@ def main():
             "dtype": "f32",
             "data": "synthetic: native triangle init, U(-0.5,0.5) angle/accel actions",
             "config": {"workload": f"{P} envs x {A} agents x {O} obstacles per GPU "
-                                   f"(BASELINE configs[2]); Env.step via C ABI",
+                                   f"({cfg_name}); Env.step via C ABI",
                        "envs_per_gpu": P, "agents": A, "obstacles": O,
                        "global_envs": world * P, "episode_len": 200,
                        "parallelism": f"independent env slices x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "kernel_us_avg": kern_avg, "kernel_us_graph": kern_graph,
-                         "kernel_us_graph_median": kern_med,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel_us": kern_us, "kernel_us_median": kern_med,
+                         "timed_region_us": region_us,
                          "alg_bytes_per_launch": launch_bytes,
                          "alg_bytes_per_env_step": per_env},
             "cpu_baseline": cpu,
@@ -251,7 +327,8 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
