@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MARLNAV_ABI_VERSION 1
+#define MARLNAV_ABI_VERSION 2
 
 /* error codes */
 #define MARLNAV_OK 0
@@ -132,10 +132,12 @@ int marlnav_step(const MarlnavDims *dims, const MarlnavParams *params,
                  const MarlnavStepBuffers *bufs, uint64_t step_idx,
                  void *stream);
 
-/* Env.observations() - environment.py:139-180. obs: (P, A, D). */
-int marlnav_observe(const MarlnavDims *dims, const float *states,
-                    const float *obstacles, const float *target, float *obs,
-                    void *stream);
+/* Env.observations() - environment.py:139-180. obs: (P, A, D). params:
+ * the env's parameters (only cap_distance, environment.py:65 / :172-177,
+ * is read); NULL means the reference's default cap 0.1. */
+int marlnav_observe(const MarlnavDims *dims, const MarlnavParams *params,
+                    const float *states, const float *obstacles,
+                    const float *target, float *obs, void *stream);
 
 /* Native TriangleIntitializer.__call__ for every env (utils.py:375-398), as
  * used by Env.__init__ (environment.py:26-30): writes states/obstacles/target
@@ -175,7 +177,7 @@ int marlnav_discounted_returns(const float *rewards, const uint8_t *done, int64_
 #define MARLNAV_FAMILY_AUTO 0
 #define MARLNAV_FAMILY_BLOCK 1 /* env-block kernel (compiled shapes)          */
 #define MARLNAV_FAMILY_SPLIT 2 /* pair-split kernel (compiled shapes)         */
-#define MARLNAV_FAMILY_TILE 3  /* wave-tile kernel (compiled shapes)          */
+/* 3 was the wave-tile family of ABI 1 (retired in ABI 2) */
 #define MARLNAV_FAMILY_WAVE 4  /* generic wave kernel (any shape)             */
 int marlnav_debug_force_family(int family);
 

@@ -11,7 +11,7 @@ fallback: if the library is missing or fails to load, ``load_library`` raises.
 import ctypes
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 FRESH_STATES_FROM_MOVED = 0x1
 NOISY_AGENTS = 0x2
@@ -77,7 +77,7 @@ def _declare(lib):
     lib.marlnav_step.argtypes = [dims_p, par_p, c.POINTER(MarlnavStepBuffers),
                                  c.c_uint64, _P]
     lib.marlnav_step.restype = c.c_int
-    lib.marlnav_observe.argtypes = [dims_p, _P, _P, _P, _P, _P]
+    lib.marlnav_observe.argtypes = [dims_p, par_p, _P, _P, _P, _P, _P]
     lib.marlnav_observe.restype = c.c_int
     lib.marlnav_reinit_all.argtypes = [dims_p, par_p, _P, _P, _P, _P, c.c_uint64, _P]
     lib.marlnav_reinit_all.restype = c.c_int

@@ -164,17 +164,17 @@ OutSet *make_set(Engine *e)
 void clear_pool(Engine *e)
 {
     if (!e->pool) return;
+    if (e->last && !e->last->pooled) {
+        e->last->release();
+        delete e->last;
+    }
+    e->last = nullptr;
     for (OutSet *s : *e->pool) {
         s->release();
         delete s;
     }
     e->pool->clear();
     e->next = 0;
-    if (e->last && !e->last->pooled) {
-        e->last->release();
-        delete e->last;
-    }
-    e->last = nullptr;
 }
 
 // The set this step writes: a pooled one nothing references any more, else
@@ -357,7 +357,8 @@ PyObject *Engine_configure(Engine *e, PyObject *args)
 }
 
 // The fast path: native re-init, default sampler, params in sync, actions
-// already an f32 contiguous (P, A, 2) tensor on the env's device. Anything
+// already an f32 contiguous 16-byte-aligned (P, A, 2) tensor on the env's
+// device. Anything
 // else goes through Env._step_py (Python), which coerces and then comes back
 // through launch().
 PyObject *Engine_call(Engine *e, PyObject *args, PyObject *kw)
@@ -373,7 +374,7 @@ PyObject *Engine_call(Engine *e, PyObject *args, PyObject *kw)
         if (t.scalar_type() == at::kFloat && t.dim() == 3 && t.is_cuda() &&
             t.get_device() == e->device && t.size(0) == e->act_shape[0] &&
             t.size(1) == e->act_shape[1] && t.size(2) == 2 && t.is_contiguous() &&
-            !t.requires_grad())
+            !t.requires_grad() && (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15u) == 0)
             return do_launch(e, t.data_ptr(), nullptr, 0);
     }
     return PyObject_CallOneArg(e->slow_step, a);

@@ -6,16 +6,13 @@
 // terminal logic, the masked re-initialisation of finished envs and the
 // recomputed observations of those envs.
 //
-// Four kernel families, one launch per step, picked on the host
+// Three kernel families, one launch per step, picked on the host
 // by shape and grid size (marlnav_step, end of file):
 //   block_kernel  - one workgroup of A waves per 64 consecutive envs, lane =
 //                   env, wave = agent (the compiled A3 shapes; the headline
 //                   path), section "env-block kernel";
 //   split_kernel  - LPR lanes per agent row, wave-private tiles (A16/O32, and
 //                   small A3 grids), section "pair-split kernel";
-//   tile_kernel   - wave tiles of 64/A envs, one lane per agent row (the
-//                   compiled shapes when a buffer misses the block kernel's
-//                   alignment);
 //   wave_kernel   - generic runtime shapes.
 // All stage their inputs in LDS with LDS-DMA, keep a lane's own row in
 // registers, assemble the packed observation rows in LDS where they stream
@@ -441,44 +438,54 @@ __device__ __forceinline__ float native_uniform(uint64_t seed, uint64_t gid, uin
     return (float)(r >> 8) * 0x1.0p-24f;
 }
 
-// native TriangleIntitializer draw for one env (utils.py:375-398)
-template <bool NOISY>
+// _reinit_update (environment.py:86-90) for a finished env (mask 1):
+// 0*old + 1*fresh, so a non-finite old value stays NaN. Idempotent in the
+// old value (blend(blend(x, f), f) has blend(x, f)'s value), so readers that
+// race with an in-place blend of the same element get the same number.
+__device__ __forceinline__ float blend_in(float old, float fresh) { return 0.0f * old + fresh; }
+
+// native TriangleIntitializer draw for one env (utils.py:375-398); BLEND:
+// blended into the env's current values (a re-init), else written (the
+// initial state)
+template <bool NOISY, bool BLEND = true>
 __device__ void native_fresh_env(int A, int S, const MarlnavParams &pr,
                                  const float *__restrict__ formation, uint64_t gid,
                                  uint64_t sidx, float *st, float *ob, float *tg)
 {
+    const auto put = [](float *d, float v) { *d = BLEND ? blend_in(*d, v) : v; };
     for (int j = 0; j < S; j += 2) {  // one Philox block = 2 obstacles
         uint32_t c[4] = {(uint32_t)(j >> 1), (uint32_t)sidx, (uint32_t)gid,
                          (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
         philox4x32_10(c, (uint32_t)pr.seed, (uint32_t)(pr.seed >> 32));
-        ob[2 * j] = pr.obs_range_x * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x;
-        ob[2 * j + 1] = pr.obs_range_y * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y;
+        put(ob + 2 * j, pr.obs_range_x * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x);
+        put(ob + 2 * j + 1, pr.obs_range_y * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y);
         if (j + 1 < S) {
-            ob[2 * j + 2] = pr.obs_range_x * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x;
-            ob[2 * j + 3] = pr.obs_range_y * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y;
+            put(ob + 2 * j + 2, pr.obs_range_x * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x);
+            put(ob + 2 * j + 3, pr.obs_range_y * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y);
         }
     }
-    for (int i = 0; i < 5 * A; ++i) st[i] = formation[i];
-    tg[0] = formation[5 * A];
-    tg[1] = formation[5 * A + 1];
-    if (NOISY) {
-        const uint32_t base = (uint32_t)(2 * S);
-        for (int i = 0; i < A; ++i) {
+    put(tg, formation[5 * A]);
+    put(tg + 1, formation[5 * A + 1]);
+    for (int i = 0; i < A; ++i) {
+        float f[5];
+        for (int k = 0; k < 5; ++k) f[k] = formation[5 * i + k];
+        if (NOISY) {
+            const uint32_t base = (uint32_t)(2 * S);
             const float u1 = native_uniform(pr.seed, gid, sidx, base + 3 * i);
             const float u2 = native_uniform(pr.seed, gid, sidx, base + 3 * i + 1);
             const float u3 = native_uniform(pr.seed, gid, sidx, base + 3 * i + 2);
             const double rad = sqrt(-2.0 * log(1.0 - (double)u1));
             const double ang = 6.283185307179586 * (double)u2;
             const float z0 = (float)(rad * cos(ang)), z1 = (float)(rad * sin(ang));
-            float *s = st + 5 * i;
-            s[0] = s[0] + pr.ags_dist * (pr.noise_std * z0);
-            s[1] = s[1] + pr.ags_dist * (pr.noise_std * z1);
+            f[0] = f[0] + pr.ags_dist * (pr.noise_std * z0);
+            f[1] = f[1] + pr.ags_dist * (pr.noise_std * z1);
             float sn, c;
             sincos_k(pr.angle_range * (u3 - 0.5f), &sn, &c);
-            const float dx = s[2], dy = s[3];
-            s[2] = c * dx + (-sn) * dy;
-            s[3] = sn * dx + c * dy;
+            const float dx = f[2], dy = f[3];
+            f[2] = c * dx + (-sn) * dy;
+            f[3] = sn * dx + c * dy;
         }
+        for (int k = 0; k < 5; ++k) put(st + 5 * i + k, f[k]);
     }
 }
 
@@ -1121,12 +1128,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                     float *sts = st + 5 * A * lane;
                     float *obe = ob + 2 * S * lane;
                     float *tge = tg + 2 * lane;
-                    if (b.fresh_states) {
-                        if (!(pr.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
-                            for (int i = 0; i < 5 * A; ++i) sts[i] = b.fresh_states[e * A * 5 + i];
-                        for (int i = 0; i < 2 * S; ++i) obe[i] = b.fresh_obstacles[e * S * 2 + i];
-                        tge[0] = b.fresh_target[2 * e];
-                        tge[1] = b.fresh_target[2 * e + 1];
+                    if (b.fresh_states) {  // fresh = the moved state itself when FROM_MOVED
+                        const bool moved = (pr.flags & MARLNAV_FRESH_STATES_FROM_MOVED) != 0;
+                        for (int i = 0; i < 5 * A; ++i)
+                            sts[i] = blend_in(sts[i], moved ? sts[i] : b.fresh_states[e * A * 5 + i]);
+                        for (int i = 0; i < 2 * S; ++i)
+                            obe[i] = blend_in(obe[i], b.fresh_obstacles[e * S * 2 + i]);
+                        tge[0] = blend_in(tge[0], b.fresh_target[2 * e]);
+                        tge[1] = blend_in(tge[1], b.fresh_target[2 * e + 1]);
                     } else {
                         native_fresh_env<NOISY>(A, S, pr, b.formation,
                                                 (uint64_t)(args.env_offset + e), args.step_idx,
@@ -1135,7 +1144,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                     for (int i = 0; i < 2 * S; ++i) b.obstacles[e * S * 2 + i] = obe[i];
                     b.target[2 * e] = tge[0];
                     b.target[2 * e + 1] = tge[1];
-                    step_num = 0.0f;
+                    step_num = blend_in(step_num, 0.0f);
                 }
                 out_st(&b.step_num[e], step_num);
                 envbits[lane] = fin ? 1u : 0u;
@@ -1329,445 +1338,6 @@ __device__ __forceinline__ void copy_span(const T *__restrict__ src, T *__restri
 
 __host__ __device__ constexpr int tile_envs(int A) { return (64 / A) >= 4 ? (64 / A) & ~3 : 64 / A; }
 
-__host__ __device__ constexpr int tile_kernel_envs(int A, int rpl) { return rpl * tile_envs(A); }
-
-// Wave tile of the tile kernels: W = RPL * tile_envs(A) envs; lane l < L
-// (L = tile_envs(A) * A) owns agent rows l, l + L, ... (RPL of them; the
-// same agent index in each, as L % A == 0), and lane e < W owns env e in the
-// per-env phase.
-template <int A, int O, int RPL_ = 1>
-struct TilePlan {
-    static constexpr int RPL = RPL_;
-    static constexpr int L = tile_envs(A) * A;
-    static constexpr int W = RPL * tile_envs(A), R = W * A, D = 2 + 2 * O + 2 * (A - 1);
-    // staging buffer (floats, 16-byte aligned regions)
-    static constexpr int ST = 0;                                  // (R, 5)
-    static constexpr int ACT = (ST + R * 5 + 3) & ~3;             // (R, 2)
-    static constexpr int OB = (ACT + R * 2 + 3) & ~3;             // (W, O, 2)
-    static constexpr int TG = (OB + W * O * 2 + 3) & ~3;          // (W, 2)
-    static constexpr int SN = (TG + W * 2 + 3) & ~3;              // (W,)
-    static constexpr int TM = (SN + W + 3) & ~3;                  // (W,) bytes
-    static constexpr int STAGE = (TM + (W + 3) / 4 + 3) & ~3;
-    static constexpr int RED = STAGE;                             // (R, 4)
-    static constexpr int FORM = RED + 4 * R;                      // 5A + 2 (native re-init)
-    static constexpr int LIST = (FORM + 5 * A + 2 + 3) & ~3;      // (W,) finished envs
-    static constexpr int FLOATS = (LIST + W + 3) & ~3;
-    // re-observed rows reuse RED once the env phase has read it: this many
-    // finished envs' (A, D) rows per chunk
-    static constexpr int REOBS_ENVS = (4 * R) / (A * D) > 0 ? (4 * R) / (A * D) : 1;
-    static_assert((4 * R) / (A * D) > 0, "RED must hold one env's re-observed rows");
-    static_assert(W <= 64, "one lane per env in the per-env phase");
-};
-
-// Re-observation of the finished envs' rows (environment.py:105) spread over
-// the wave: one (row, pair) item per lane per pass instead of one whole row
-// per lane, so a tile with a few finished envs pays about one pair's latency
-// instead of a row's. st/ob/tg: the tile's re-initialised LDS state; list:
-// the tile indices of the nfin finished envs (this chunk); results go to
-// obsr[(rank * A + agent) * D + slot] in the packed Observations order.
-template <int A, int O, bool FAST>
-__device__ __forceinline__ void reobs_spread(const float *st, const float *ob, const float *tg,
-                                             const int *list, int nfin, float *obsr, float cap,
-                                             unsigned lane)
-{
-    constexpr int NP = 1 + O + (A - 1), D = 2 + 2 * O + 2 * (A - 1);
-    const int nw = nfin * A * NP;
-    for (int base = 0; base < nw; base += 64) {
-        const int w = base + (int)lane;
-        if (w < nw) {
-            const int fe = w / (A * NP), rem = w - fe * (A * NP);
-            const int ag = rem / NP, p = rem - ag * NP;
-            const int env = list[fe];
-            const int row = env * A + ag;
-            const float *s = st + 5 * row;
-            const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
-            const float *pt;
-            int sa, sd;
-            if (p == 0) {                 // target
-                pt = tg + 2 * env;
-                sa = 0;
-                sd = 1;
-            } else if (p <= O) {          // obstacle p - 1
-                pt = ob + 2 * (env * O + p - 1);
-                sa = 1 + p;
-                sd = 1 + O + p;
-            } else {                      // other agent k, skipping self
-                const int kx = p - O - 1;
-                pt = st + 5 * (env * A + kx + (kx >= ag ? 1 : 0));
-                sa = 2 + 2 * O + kx;
-                sd = 2 + 2 * O + (A - 1) + kx;
-            }
-            bool unused = true;
-            const float px = pt[0], py = pt[1];
-            const float d = pair_dist<FAST>(ox, oy, px, py, unused);
-            float *o = obsr + (fe * A + ag) * D;
-            o[sa] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, unused);
-            o[sd] = d;
-        }
-    }
-}
-
-// Stage tile `tile` into `buf`: LDS-DMA for a full tile (returns without
-// waiting), plain copies for a partial last tile.
-template <int A, int O, bool OBS_ONLY, int RPL>
-__device__ __forceinline__ void tile_stage(const StepPtrs &b, int64_t P, int64_t tile,
-                                           float *buf, unsigned lane)
-{
-    using TP = TilePlan<A, O, RPL>;
-    constexpr int W = TP::W, R = TP::R;
-    const int64_t e0 = tile * W;
-    if (P - e0 >= W) {
-        glds_span<R * 20>(b.states + e0 * (A * 5), buf + TP::ST, lane);
-        if (!OBS_ONLY) glds_span<R * 8>(b.actions + e0 * (A * 2), buf + TP::ACT, lane);
-        glds_span<W * O * 8>(b.obstacles + e0 * (O * 2), buf + TP::OB, lane);
-        glds_span<W * 8>(b.target + e0 * 2, buf + TP::TG, lane);
-        if (!OBS_ONLY) {
-            glds_span<W * 4>(b.step_num + e0, buf + TP::SN, lane);
-            glds_span<W>(b.terminates + e0, buf + TP::TM, lane);
-        }
-        // native re-init template (utils.py:375-398): a finished env copies it
-        // from LDS instead of waiting on a global load
-        if (!OBS_ONLY && b.formation) glds_span<(5 * A + 2) * 4>(b.formation, buf + TP::FORM, lane);
-    } else {
-        const int ne = (int)(P - e0), nr = ne * A;
-        copy_span(b.states + e0 * (A * 5), buf + TP::ST, nr * 5, (int)lane);
-        if (!OBS_ONLY) copy_span(b.actions + e0 * (A * 2), buf + TP::ACT, nr * 2, (int)lane);
-        copy_span(b.obstacles + e0 * (O * 2), buf + TP::OB, ne * O * 2, (int)lane);
-        copy_span(b.target + e0 * 2, buf + TP::TG, ne * 2, (int)lane);
-        if (!OBS_ONLY) {
-            copy_span(b.step_num + e0, buf + TP::SN, ne, (int)lane);
-            copy_span(b.terminates + e0, reinterpret_cast<uint8_t *>(buf + TP::TM), ne, (int)lane);
-            if (b.formation) copy_span(b.formation, buf + TP::FORM, 5 * A + 2, (int)lane);
-        }
-    }
-}
-
-// One wave per tile: stage by LDS-DMA, move, observe, reward/terminal logic,
-// re-init and re-observe finished envs, stream out. Each lane's RPL rows are
-// independent work the compiler interleaves: RPL = 1 gives the most waves
-// (shortest per-wave chain; best while the grid is one round of waves),
-// RPL = 2 halves the per-env fixed cost (best once waves queue up).
-template <int A, int O, bool OBS_ONLY, bool NOISY, int RPL>
-__global__ void __launch_bounds__(64 * kWavesPerBlock) tile_kernel(KArgs k)
-{
-    using TP = TilePlan<A, O, RPL>;
-    constexpr int W = TP::W, D = TP::D, L = TP::L;
-    (void)k;  // read through kargs_late()
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-#if MARLNAV_ABLATE & 64
-    return;  // launch-overhead probe
-#endif
-#if MARLNAV_STAMPS
-    unsigned long long t_entry;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
-#endif
-    const unsigned lane = threadIdx.x & 63;
-    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wib;
-    const int64_t tile = gw;
-    KArgsK *K = kargs_late();
-    const int64_t P = K->a.P;
-    // pointers first, pinned in SGPRs before the exit test: one round of
-    // kernarg loads ahead of the first wait (the compiler would otherwise
-    // sink them below the branch, a second serial round)
-    const StepPtrs b = load_ptrs(K);
-    const int64_t ntiles = K->a.ntiles;
-    asm volatile("" ::"s"(b.states), "s"(b.obstacles), "s"(b.target), "s"(b.actions),
-                 "s"(b.obs), "s"(ntiles), "s"(P));
-    if (tile >= ntiles) return;
-    STAMP(0);
-    float *wl = lds + wib * TP::FLOATS;
-    float *cur = wl;
-    float4 *red = reinterpret_cast<float4 *>(wl + TP::RED);
-    tile_stage<A, O, OBS_ONLY, RPL>(b, P, tile, cur, lane);
-    const MarlnavParams pr = load_params(K);
-    const int el = (int)lane / A, a = (int)lane - el * A;
-    unsigned c_trunc = 0, c_col = 0, c_tar = 0;
-    unsigned n_fin = 0;  // finished envs of this tile (stamps builds record it)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
-    wave_sync();
-    STAMP(1);
-    {
-        const int64_t e0 = tile * W;
-        const int ne = (int)((P - e0) < W ? (P - e0) : W);
-        const int nr = ne * A;
-        const bool env_on = (int)lane < ne;
-        float *st = cur + TP::ST;
-        // row k of this lane: index lane + k*L, env el + k*(L/A)
-        bool row_on[RPL];
-        int rix[RPL], rel[RPL];
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            rix[q] = (int)lane + q * L;
-            rel[q] = el + q * (L / A);
-            row_on[q] = (int)lane < L && rix[q] < nr;
-        }
-
-        // ---- _move_agents (environment.py:113-123), own rows in registers
-        float ox[RPL], oy[RPL], dx[RPL], dy[RPL];
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            const float *s = st + 5 * rix[q];
-            ox[q] = s[0];
-            oy[q] = s[1];
-            dx[q] = s[2];
-            dy[q] = s[3];
-        }
-        if (!OBS_ONLY) {
-#pragma unroll
-            for (int q = 0; q < RPL; ++q) {
-                const float2 act = reinterpret_cast<const float2 *>(cur + TP::ACT)[rix[q]];
-                float a0 = act.x, a1 = act.y;
-                if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
-                    KArgsK *kl = kargs_late();
-                    a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
-                    a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
-                }
-                float sn, c;
-                sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
-                const float ndx = c * dx[q] + (-sn) * dy[q];
-                const float ndy = sn * dx[q] + c * dy[q];
-                float *s = st + 5 * rix[q];
-                const float v = clamp_t(s[4] + clamp_t(a1, pr.min_accel, pr.max_accel),
-                                        pr.min_speed, pr.max_speed);
-                ox[q] = ox[q] + ndx * v;
-                oy[q] = oy[q] + ndy * v;
-                dx[q] = ndx;
-                dy[q] = ndy;
-                if (row_on[q]) {
-                    s[0] = ox[q];
-                    s[1] = oy[q];
-                    s[2] = dx[q];
-                    s[3] = dy[q];
-                    s[4] = v;
-                }
-            }
-            wave_sync();
-        }
-        STAMP(2);
-
-        // ---- observations of the moved state + reward terms (:99-100)
-        float rowv[RPL][D];
-        // wave-uniform choice of the pair math: the short sqrt / shared-
-        // reciprocal division sequences when every coordinate of the tile
-        // passes coord_ok (then they equal the IEEE results), IEEE otherwise
-        bool cok = true;
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) cok = cok && (!row_on[q] || (coord_ok(ox[q]) && coord_ok(oy[q])));
-        cok = cok && tile_coords_ok<W * O * 2, W * 2>(cur + TP::OB, cur + TP::TG, lane);
-        const bool fast = ne == W && __ballot(!cok) == 0ull;
-        if (!(MARLNAV_ABLATE & 16) && (int)lane < L) {
-            RowOut ro[RPL];
-            if (__builtin_expect(fast, 1)) {
-#pragma unroll
-                for (int q = 0; q < RPL; ++q) {
-                    bool unused = true;  // guards implied by coords_in_range
-                    ro[q] = observe_row_own<A, O, !OBS_ONLY, true>(
-                        st + 5 * A * rel[q], cur + TP::OB + 2 * O * rel[q],
-                        cur + TP::TG + 2 * rel[q], a, ox[q], oy[q], dx[q], dy[q], rowv[q], pr,
-                        unused);
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < RPL; ++q) {
-                    bool unused = true;
-                    ro[q] = observe_row_own<A, O, !OBS_ONLY, false>(
-                        st + 5 * A * rel[q], cur + TP::OB + 2 * O * rel[q],
-                        cur + TP::TG + 2 * rel[q], a, ox[q], oy[q], dx[q], dy[q], rowv[q], pr,
-                        unused);
-                }
-            }
-            if (!OBS_ONLY) {
-#pragma unroll
-                for (int q = 0; q < RPL; ++q)
-                    if (row_on[q])
-                        red[rix[q]] = make_float4(ro[q].r_miss, ro[q].r_hit,
-                                                  __uint_as_float(ro[q].flags), 0.0f);
-            }
-        }
-
-        STAMP(3);
-        if (!OBS_ONLY) {
-            wave_sync();
-            // ---- per-env reductions, terminal logic, masked re-init
-            bool fin = false, tr_l = false, co_l = false, ta_l = false;
-            if (env_on) {
-                const int64_t e = e0 + lane;
-                float4 rr[A];
-#pragma unroll
-                for (int i = 0; i < A; ++i) rr[i] = red[A * lane + i];
-                unsigned any_col = 0u, all_in = 1u;
-#pragma unroll
-                for (int i = 0; i < A; ++i) {
-                    const unsigned f = __float_as_uint(rr[i].z);
-                    any_col |= f & 1u;
-                    all_in &= (f >> 1) & 1u;
-                }
-                float rv[A];
-#pragma unroll
-                for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
-                const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
-                bool okq = MARLNAV_FM_TERMS != 0;                                    // torch.mean (:233)
-                float rmean = MARLNAV_FM_TERMS ? div_c(rsum, make_divc((float)A, okq), okq) : 0.0f;
-                if (__builtin_expect(!okq, 0)) rmean = rsum / (float)A;
-                out_st(&b.reward[e], rmean);
-
-                float step_num = cur[TP::SN + lane] + 1.0f;        // :96
-                const bool truncated = step_num > pr.trunc_after;  // :97
-                const bool term_old = reinterpret_cast<const uint8_t *>(cur + TP::TM)[lane] != 0;
-                const bool terminated = any_col || term_old;       // :213-214
-                out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
-                out_st(&b.terminated[e], (uint8_t)terminated);
-                out_st(&b.truncated[e], (uint8_t)truncated);
-                fin = truncated || terminated;                     // :102-104
-                if (fin) {
-                    KArgsK *kl = kargs_late();
-                    MarlnavParams p;  // the fields the re-init reads
-                    p.obs_range_x = kl->p.obs_range_x;
-                    p.obs_mean_x = kl->p.obs_mean_x;
-                    p.obs_range_y = kl->p.obs_range_y;
-                    p.obs_mean_y = kl->p.obs_mean_y;
-                    p.ags_dist = kl->p.ags_dist;
-                    p.noise_std = kl->p.noise_std;
-                    p.angle_range = kl->p.angle_range;
-                    p.flags = kl->p.flags;
-                    p.seed = kl->p.seed;
-                    float *s5 = st + 5 * A * lane;
-                    float *obl = cur + TP::OB + 2 * O * lane;
-                    float *tgl = cur + TP::TG + 2 * lane;
-                    const float *fs = kl->a.b.fresh_states;
-                    float *gob = kl->a.b.obstacles;
-                    float *gtg = kl->a.b.target;
-                    if (fs) {
-                        const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
-                        if (!(p.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
-                            for (int i = 0; i < 5 * A; ++i) s5[i] = fs[e * A * 5 + i];
-                        for (int i = 0; i < 2 * O; ++i) obl[i] = fo[e * O * 2 + i];
-                        tgl[0] = ft[2 * e];
-                        tgl[1] = ft[2 * e + 1];
-                    } else {
-                        native_fresh_env<NOISY>(A, O, p, cur + TP::FORM,
-                                                (uint64_t)(kl->a.env_offset + e), kl->a.step_idx,
-                                                s5, obl, tgl);
-                    }
-                    for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
-                    gtg[2 * e] = tgl[0];
-                    gtg[2 * e + 1] = tgl[1];
-                    step_num = 0.0f;
-                }
-                out_st(&b.step_num[e], step_num);
-                tr_l = truncated;
-                co_l = any_col;
-                ta_l = all_in;
-            }
-            const uint64_t finmask = __ballot(fin);
-            n_fin = __popcll(finmask);
-            c_trunc += __popcll(__ballot(tr_l));
-            c_col += __popcll(__ballot(co_l));
-            c_tar += __popcll(__ballot(ta_l));
-            STAMP(4);
-
-            // ---- observations of re-initialised envs (:105)
-            if (finmask) {
-                int *list = reinterpret_cast<int *>(cur + TP::LIST);
-                if (fin)
-                    list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] =
-                        (int)lane;
-                wave_sync();
-                bool cok2 = true;
-#pragma unroll
-                for (int q = 0; q < RPL; ++q)
-                    cok2 = cok2 && (!row_on[q] || (coord_ok(st[5 * rix[q]]) &&
-                                                   coord_ok(st[5 * rix[q] + 1])));
-                cok2 = cok2 && tile_coords_ok<W * O * 2, W * 2>(cur + TP::OB, cur + TP::TG, lane);
-                const bool fast2 = ne == W && __ballot(!cok2) == 0ull;
-                const int nfin = (int)__popcll(finmask);
-                float *obsr = cur + TP::RED;  // free once the env phase has read it
-                int rank[RPL];
-#pragma unroll
-                for (int q = 0; q < RPL; ++q)
-                    rank[q] = (int)__popcll(finmask & ((1ull << rel[q]) - 1ull));
-                for (int c0 = 0; c0 < nfin; c0 += TP::REOBS_ENVS) {
-                    const int nc = nfin - c0 < TP::REOBS_ENVS ? nfin - c0 : TP::REOBS_ENVS;
-                    if (fast2)
-                        reobs_spread<A, O, true>(st, cur + TP::OB, cur + TP::TG, list + c0, nc,
-                                                 obsr, pr.cap_distance, lane);
-                    else
-                        reobs_spread<A, O, false>(st, cur + TP::OB, cur + TP::TG, list + c0, nc,
-                                                  obsr, pr.cap_distance, lane);
-                    wave_sync();
-#pragma unroll
-                    for (int q = 0; q < RPL; ++q)
-                        if (row_on[q] && ((finmask >> rel[q]) & 1u) && rank[q] >= c0 &&
-                            rank[q] < c0 + nc) {
-                            const float *o = obsr + ((rank[q] - c0) * A + a) * D;
-#pragma unroll
-                            for (int j = 0; j < D; ++j) rowv[q][j] = o[j];
-                        }
-                    wave_sync();
-                }
-            }
-        }
-
-        STAMP(5);
-        // ---- stream the tile out
-        float *obase = in_sgpr(b.obs + e0 * (A * D));
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            if (row_on[q]) {
-                store_row<D>(obase + rix[q] * D, rowv[q]);
-                if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
-                    KArgsK *kl = kargs_late();
-                    const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
-                    float nv[D];
-#pragma unroll
-                    for (int j = 0; j < D; ++j) nv[j] = (rowv[q][j] - mean[j]) / scale[j];
-                    store_row<D>(kl->a.b.obs_norm + (e0 * A + rix[q]) * D, nv);
-                }
-            }
-        }
-        if (!OBS_ONLY) {
-            wave_sync();
-            float *gst = in_sgpr(b.states + e0 * (A * 5));
-            if (ne == W) {
-                constexpr int N16 = TP::R * 5 / 4;  // R*5 is a multiple of 4 (W % 4 == 0)
-#pragma unroll
-                for (int kk = 0; kk * 64 < N16; ++kk) {
-                    const int i = kk * 64 + (int)lane;
-                    if ((kk + 1) * 64 <= N16 || i < N16)
-                        out_st4(gst + 4 * i, reinterpret_cast<const float4 *>(st)[i]);
-                }
-            } else {
-                for (int i = (int)lane; i < nr * 5; i += 64) out_st(gst + i, st[i]);
-            }
-        }
-    }
-    STAMP(6);
-    if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
-        // this wave's own slots: contention-free, fire-and-forget
-        KArgsK *kl = kargs_late();
-        uint64_t *cnt = kl->a.b.counters;
-        const int64_t slots = kl->a.waves;
-        if (cnt) {
-            const int64_t sl = gw % slots;  // slots may be fewer than this grid's waves
-            if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
-            if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + sl], (unsigned long long)c_col);
-            if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
-        }
-    }
-#if MARLNAV_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    STAMP(7);
-    if (lane == 0) {
-        g_stamps[(size_t)gw * 24 + 16] = t_entry;
-        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
-        g_stamps[(size_t)gw * 24 + 19] = n_fin;
-    }
-#endif
-    (void)n_fin;
-}
 
 // ------------------------------------------------------ pair-split kernel
 // For shapes whose rows carry many pairs (A16/O32: 48 per row) or grids too
@@ -1934,16 +1504,19 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
             const int c = list[fe];
             const int64_t e = ev.env(c);
             if (kk < 5 * A) {
-                if (!keep) ev.state(c)[kk] = fs[e * A * 5 + kk];
+                float *d = ev.state(c) + kk;
+                *d = blend_in(*d, keep ? *d : fs[e * A * 5 + kk]);
             } else if (kk < 5 * A + 2 * O) {
                 const int j = kk - 5 * A;
-                const float v = fo[e * O * 2 + j];
-                ev.obst(c)[j] = v;
+                float *d = ev.obst(c) + j;
+                const float v = blend_in(*d, fo[e * O * 2 + j]);
+                *d = v;
                 gob[e * O * 2 + j] = v;
             } else {
                 const int j = kk - 5 * A - 2 * O;
-                const float v = ft[2 * e + j];
-                ev.targ(c)[j] = v;
+                float *d = ev.targ(c) + j;
+                const float v = blend_in(*d, ft[2 * e + j]);
+                *d = v;
                 gtg[2 * e + j] = v;
             }
         }
@@ -1959,11 +1532,14 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
         const int c = list[fe];
         const int64_t e = ev.env(c);
         if (kk < 5 * A) {
-            ev.state(c)[kk] = form[kk];
+            float *d = ev.state(c) + kk;
+            *d = blend_in(*d, form[kk]);
         } else if (kk < 5 * A + 2) {
             const int j = kk - 5 * A;
-            ev.targ(c)[j] = form[kk];
-            gtg[2 * e + j] = form[kk];
+            float *d = ev.targ(c) + j;
+            const float v = blend_in(*d, form[kk]);
+            *d = v;
+            gtg[2 * e + j] = v;
         } else {
             const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
             const uint64_t gid = (uint64_t)(eoff + e);
@@ -1973,11 +1549,11 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
             const int j = 2 * jb;
             float *o = ev.obst(c) + 2 * j;
             float *g = gob + e * O * 2 + 2 * j;
-            o[0] = g[0] = rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-            o[1] = g[1] = ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
+            o[0] = g[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+            o[1] = g[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
             if (j + 1 < O) {
-                o[2] = g[2] = rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-                o[3] = g[3] = ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
+                o[2] = g[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+                o[3] = g[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
             }
         }
     }
@@ -2034,27 +1610,35 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
             philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
         }
         if (pair) {
+            // inputs: the blend of the env's current value (LDS; other items
+            // may be blending it in place meanwhile - blend_in is idempotent)
+            // with its fresh value (template or Philox draw)
             const float *s = form + 5 * ag;
-            const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
+            const float *so = ev.state(c) + 5 * ag;
+            const float ox = blend_in(so[0], s[0]), oy = blend_in(so[1], s[1]);
+            const float dx = blend_in(so[2], s[2]), dy = blend_in(so[3], s[3]);
             float px, py;
             int sa, sd;
             if (p == 0) {            // target
-                px = form[5 * A];
-                py = form[5 * A + 1];
+                px = blend_in(ev.targ(c)[0], form[5 * A]);
+                py = blend_in(ev.targ(c)[1], form[5 * A + 1]);
                 sa = 0;
                 sd = 1;
             } else if (p <= O) {     // obstacle p - 1: components of its Philox block
                 const bool hi = ((p - 1) & 1) != 0;
                 const uint32_t ux = hi ? cc[2] : cc[0], uy = hi ? cc[3] : cc[1];
-                px = rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx;
-                py = ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my;
+                const float *oo = ev.obst(c) + 2 * (p - 1);
+                px = blend_in(oo[0], rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx);
+                py = blend_in(oo[1], ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my);
                 sa = 1 + p;
                 sd = 1 + O + p;
             } else {                 // other agent kx, skipping self
                 const int kx = p - O - 1;
-                const float *q = form + 5 * (kx + (kx >= ag ? 1 : 0));
-                px = q[0];
-                py = q[1];
+                const int m = kx + (kx >= ag ? 1 : 0);
+                const float *q = form + 5 * m;
+                const float *qo = ev.state(c) + 5 * m;
+                px = blend_in(qo[0], q[0]);
+                py = blend_in(qo[1], q[1]);
                 sa = 2 + 2 * O + kx;
                 sd = 2 + 2 * O + (A - 1) + kx;
             }
@@ -2076,20 +1660,23 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
         } else if (on) {
             const int k2 = kk - NPAIR;
             if (k2 < 5 * A) {
-                ev.state(c)[k2] = form[k2];
+                float *d = ev.state(c) + k2;
+                *d = blend_in(*d, form[k2]);
             } else if (k2 < 5 * A + 2) {
                 const int j = k2 - 5 * A;
-                ev.targ(c)[j] = form[k2];
-                gtg[2 * e + j] = form[k2];
+                float *d = ev.targ(c) + j;
+                const float v = blend_in(*d, form[k2]);
+                *d = v;
+                gtg[2 * e + j] = v;
             } else {
                 const int j = 2 * jb;
                 float *o = ev.obst(c) + 2 * j;
                 float *g = gob + e * O * 2 + 2 * j;
-                o[0] = g[0] = rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-                o[1] = g[1] = ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
+                o[0] = g[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+                o[1] = g[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
                 if (j + 1 < O) {
-                    o[2] = g[2] = rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-                    o[3] = g[3] = ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
+                    o[2] = g[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+                    o[3] = g[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
                 }
             }
         }
@@ -2428,7 +2015,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
     float *orow = wl + SP::OBS + rowc * SP::DP;
     float *brow = wl + SP::BOND + rowc * (A - 1);
     {
-        // wave-uniform choice of the pair math (coord_ok, as in tile_kernel);
+        // wave-uniform choice of the pair math (coord_ok);
         // worth its check only when each lane evaluates many pairs
         bool fast = false;
         if constexpr (kSplitFastMath<A, O, LPR>) {
@@ -2545,11 +2132,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
                 float *gtg = kl->a.b.target;
                 if (!NOISY && fs) {
                     const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
-                    if (!(p.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
-                        for (int i = 0; i < 5 * A; ++i) s5[i] = fs[e * A * 5 + i];
-                    for (int i = 0; i < 2 * O; ++i) obl[i] = fo[e * O * 2 + i];
-                    tgl[0] = ft[2 * e];
-                    tgl[1] = ft[2 * e + 1];
+                    const bool moved = (p.flags & MARLNAV_FRESH_STATES_FROM_MOVED) != 0;
+                    for (int i = 0; i < 5 * A; ++i)
+                        s5[i] = blend_in(s5[i], moved ? s5[i] : fs[e * A * 5 + i]);
+                    for (int i = 0; i < 2 * O; ++i) obl[i] = blend_in(obl[i], fo[e * O * 2 + i]);
+                    tgl[0] = blend_in(tgl[0], ft[2 * e]);
+                    tgl[1] = blend_in(tgl[1], ft[2 * e + 1]);
                 } else {
                     native_fresh_env<NOISY>(A, O, p, kl->a.b.formation,
                                             (uint64_t)(kl->a.env_offset + e), kl->a.step_idx, s5,
@@ -2559,7 +2147,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) MARLNAV_SPLIT_WPE_ATTR sp
                 gtg[2 * e] = tgl[0];
                 gtg[2 * e + 1] = tgl[1];
             }
-            if (fin) step_num = 0.0f;
+            if (fin) step_num = blend_in(step_num, 0.0f);
             out_st(&b.step_num[e], step_num);
             tr_l = truncated;
             co_l = any_col;
@@ -3027,23 +2615,9 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
                 out_st(&b.terminated[e], (uint8_t)terminated);
                 out_st(&b.truncated[e], (uint8_t)truncated);
                 fin = truncated || terminated;                     // :102-104
-                if ((NOISY || !kBlkSpread) && fin) {  // serial re-init per env
+                if (NOISY && fin) {  // noisy native re-init: serial per env
                     KArgsK *kl = kargs_late();
-                    if (!NOISY && kl->a.b.fresh_states) {
-                        float *s5 = st + 5 * A * l;
-                        float *obl = lds + BP::OB + 2 * O * l;
-                        float *tgl = lds + BP::TG + 2 * l;
-                        const float *fs = kl->a.b.fresh_states;
-                        const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
-                        if (!(kl->p.flags & MARLNAV_FRESH_STATES_FROM_MOVED))
-                            for (int i = 0; i < 5 * A; ++i) s5[i] = fs[e * A * 5 + i];
-                        for (int i = 0; i < 2 * O; ++i) obl[i] = fo[e * O * 2 + i];
-                        tgl[0] = ft[2 * e];
-                        tgl[1] = ft[2 * e + 1];
-                        for (int i = 0; i < 2 * O; ++i) kl->a.b.obstacles[e * O * 2 + i] = obl[i];
-                        kl->a.b.target[2 * e] = tgl[0];
-                        kl->a.b.target[2 * e + 1] = tgl[1];
-                    } else {
+                    {
                         MarlnavParams p;  // the fields the re-init reads
                         p.obs_range_x = kl->p.obs_range_x;
                         p.obs_mean_x = kl->p.obs_mean_x;
@@ -3065,7 +2639,7 @@ __global__ void __launch_bounds__(64 * A) MARLNAV_BLOCK_WPE_ATTR block_kernel(KA
                         kl->a.b.target[2 * e + 1] = tgl[1];
                     }
                 }
-                out_st(&b.step_num[e], fin ? 0.0f : step_num);
+                out_st(&b.step_num[e], fin ? blend_in(step_num, 0.0f) : step_num);
                 tr_l = truncated;
                 co_l = any_col;
                 ta_l = all_in;
@@ -3197,10 +2771,10 @@ __global__ void reinit_all_kernel(int64_t P, int A, int S, int64_t env_offset, u
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= P) return;
     if (pr.flags & MARLNAV_NOISY_AGENTS)
-        native_fresh_env<true>(A, S, pr, formation, (uint64_t)(env_offset + e), sidx,
+        native_fresh_env<true, false>(A, S, pr, formation, (uint64_t)(env_offset + e), sidx,
                                states + e * A * 5, obstacles + e * S * 2, target + 2 * e);
     else
-        native_fresh_env<false>(A, S, pr, formation, (uint64_t)(env_offset + e), sidx,
+        native_fresh_env<false, false>(A, S, pr, formation, (uint64_t)(env_offset + e), sidx,
                                 states + e * A * 5, obstacles + e * S * 2, target + 2 * e);
 }
 
@@ -3288,72 +2862,10 @@ const KernelPair kVariants[] = {
      wave_kernel<16, 32, false, true>},
 };
 
-// LDS-DMA tile kernels (tile_kernel) for these shapes; MARLNAV_TILE=0 builds
-// without them (A/B timing against wave_kernel)
-#ifndef MARLNAV_TILE
-#define MARLNAV_TILE 1
-#endif
+// Step kernels that take their arguments through one KArgs block
 using TileFn = void (*)(KArgs);
-// RPL=1 waves (one per 64/A-env tile) from which RPL=2 is used
-constexpr int64_t kRpl2Waves = 49152;  // measured crossover ~0.5-1M envs at A=3
-
-struct TileSet {
-    TileFn step, obs, noisy;
-    size_t lds;  // bytes per block
-};
-
-struct TilePair {
-    int A, O;
-    TileSet rpl[2];  // 1 and 2 rows per lane
-};
-
-#define MARLNAV_TILE_SET(A, O, R)                                                   \
-    {tile_kernel<A, O, false, false, R>, tile_kernel<A, O, true, false, R>,         \
-     tile_kernel<A, O, false, true, R>, (size_t)TilePlan<A, O, R>::FLOATS * 4 * kWavesPerBlock}
-#define MARLNAV_TILE_VARIANT(A, O) \
-    {A, O, {MARLNAV_TILE_SET(A, O, 1), MARLNAV_TILE_SET(A, O, 2)}}
-const TilePair kTileVariants[] = {
-    MARLNAV_TILE_VARIANT(3, 3),
-    MARLNAV_TILE_VARIANT(3, 8),
-    MARLNAV_TILE_VARIANT(3, 1),
-    MARLNAV_TILE_VARIANT(2, 1),
-};
-#undef MARLNAV_TILE_VARIANT
-#undef MARLNAV_TILE_SET
-
-// rows per lane for a launch: 2 once the RPL=1 grid is several rounds of
-// waves (MARLNAV_RPL=1|2 forces one, for tuning)
-int pick_rpl(int64_t P, int A)
-{
-    static const int forced = [] {
-        const char *v = getenv("MARLNAV_RPL");
-        return v ? (int)strtol(v, nullptr, 10) : 0;
-    }();
-    if (forced == 1 || forced == 2) return forced;
-    const int64_t waves1 = (P + tile_envs(A) - 1) / tile_envs(A);
-    return waves1 >= kRpl2Waves ? 2 : 1;
-}
 
 bool aligned(const void *p, uintptr_t n) { return (reinterpret_cast<uintptr_t>(p) & (n - 1)) == 0; }
-
-// tile_kernel applies: a compiled shape, obstacle_stride == O and the
-// alignment its LDS-DMA staging and vector stores assume
-const TilePair *select_tile(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only)
-{
-    if (!MARLNAV_TILE || d->obstacle_stride != d->num_obstacles) return nullptr;
-    const TilePair *t = nullptr;
-    for (const TilePair &v : kTileVariants)
-        if (v.A == d->num_agents && v.O == d->num_obstacles) t = &v;
-    if (!t || tile_envs(t->A) != pick_wave_envs(t->A, t->O, t->O)) return nullptr;
-    if (tile_kernel_envs(t->A, 2) % 4 != 0) return nullptr;
-    if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
-        !aligned(b.obs, 16))
-        return nullptr;
-    if (!obs_only && (!aligned(b.actions, 16) || !aligned(b.step_num, 16) ||
-                      !aligned(b.terminates, 4)))
-        return nullptr;
-    return t;
-}
 
 // pair-split kernels (split_kernel): rows with many pairs, or grids too small
 // for one lane per row to fill the chip
@@ -3397,11 +2909,7 @@ constexpr int64_t kSplitBelowWaves = 512;
 const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only,
                                  bool force_size = false)
 {
-    static const int forced = [] {
-        const char *v = getenv("MARLNAV_SPLIT");
-        return v ? (int)strtol(v, nullptr, 10) : -1;
-    }();
-    if (forced == 0 || d->obstacle_stride != d->num_obstacles) return nullptr;
+    if (d->obstacle_stride != d->num_obstacles) return nullptr;
     const SplitVariant *v = nullptr;
     for (const SplitVariant &x : kSplitVariants) {
         if (x.A != d->num_agents || x.O != d->num_obstacles) continue;
@@ -3414,7 +2922,7 @@ const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers 
     if (!v) return nullptr;
     const int64_t row_waves = (d->num_parallel + tile_envs(v->A) - 1) / tile_envs(v->A);
     const int64_t pairs = 1 + v->O + (v->A - 1);
-    if (!v->always && forced != 1 && !force_size && row_waves * 6 >= kSplitBelowWaves * pairs)
+    if (!v->always && !force_size && row_waves * 6 >= kSplitBelowWaves * pairs)
         return nullptr;
     if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
         !aligned(b.obs, 16))
@@ -3461,11 +2969,7 @@ const BlockVariant kBlockVariants[] = {
 
 const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only)
 {
-    static const int forced = [] {
-        const char *v = getenv("MARLNAV_BLOCK");
-        return v ? (int)strtol(v, nullptr, 10) : -1;
-    }();
-    if (forced == 0 || d->obstacle_stride != d->num_obstacles) return nullptr;
+    if (d->obstacle_stride != d->num_obstacles) return nullptr;
     const BlockVariant *v = nullptr;
     for (const BlockVariant &x : kBlockVariants)
         if (x.A == d->num_agents && x.O == d->num_obstacles) v = &x;
@@ -3490,26 +2994,6 @@ int launch_block(const BlockVariant &v, TileFn fn, const StepArgs &args, const M
     void *kargs[] = {&ka};
     hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)ka.a.ntiles),
                                    dim3(64 * v.A), kargs, v.lds, (hipStream_t)stream);
-    if (e == hipSuccess) e = hipGetLastError();
-    if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
-    return 0;
-}
-
-int launch_tile(TileFn fn, size_t lds, int rpl, const Launch &L, const StepArgs &args,
-                const MarlnavParams &pr, void *stream, const char *what)
-{
-    KArgs ka;
-    ka.a = args;
-    ka.p = pr;
-    // the tile kernels' own tiles (W = tile_kernel_envs(A)); the counter slot
-    // stride stays the wave_kernel count from plan_launch (>= waves here)
-    const int64_t W = tile_kernel_envs(args.A, rpl);
-    ka.a.W = (int)W;
-    ka.a.ntiles = (args.P + W - 1) / W;
-    const int64_t blocks = (ka.a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    void *kargs[] = {&ka};
-    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)blocks),
-                                   dim3(64 * kWavesPerBlock), kargs, lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
     return 0;
@@ -3652,21 +3136,13 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
             g_last_family = MARLNAV_FAMILY_BLOCK;
             return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }
-    if (family_allowed(MARLNAV_FAMILY_TILE))
-        if (const TilePair *t = select_tile(d, *b, false)) {
-            const int r = pick_rpl(d->num_parallel, d->num_agents);
-            const TileSet &ts = t->rpl[r - 1];
-            g_last_family = MARLNAV_FAMILY_TILE;
-            return launch_tile(noisy ? ts.noisy : ts.step, ts.lds, r, L, args, *pr, stream,
-                               "marlnav_step");
-        }
     const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
     g_last_family = MARLNAV_FAMILY_WAVE;
     return launch(noisy ? k.noisy : k.step, L, args, *pr, stream, "marlnav_step");
 }
 
-int marlnav_observe(const MarlnavDims *d, const float *states, const float *obstacles,
-                    const float *target, float *obs, void *stream)
+int marlnav_observe(const MarlnavDims *d, const MarlnavParams *params, const float *states,
+                    const float *obstacles, const float *target, float *obs, void *stream)
 {
     if (int rc = validate(d)) return rc;
     if (!states || !obstacles || !target || !obs)
@@ -3679,7 +3155,9 @@ int marlnav_observe(const MarlnavDims *d, const float *states, const float *obst
     args.b.obs = obs;
     MarlnavParams pr;
     memset(&pr, 0, sizeof(pr));
-    pr.cap_distance = 0.1f;  // environment.py:65
+    // the angle cap (environment.py:172-177) is the only parameter observe reads;
+    // NULL params: the reference's default (environment.py:65)
+    pr.cap_distance = params ? params->cap_distance : 0.1f;
     const bool fsplit = g_family == MARLNAV_FAMILY_SPLIT;
     if (family_allowed(MARLNAV_FAMILY_SPLIT))
         if (const SplitVariant *v = select_split(d, args.b, true, fsplit)) {
@@ -3690,13 +3168,6 @@ int marlnav_observe(const MarlnavDims *d, const float *states, const float *obst
         if (const BlockVariant *v = select_block(d, args.b, true)) {
             g_last_family = MARLNAV_FAMILY_BLOCK;
             return launch_block(*v, v->obs, args, pr, stream, "marlnav_observe");
-        }
-    if (family_allowed(MARLNAV_FAMILY_TILE))
-        if (const TilePair *t = select_tile(d, args.b, true)) {
-            const int r = pick_rpl(d->num_parallel, d->num_agents);
-            g_last_family = MARLNAV_FAMILY_TILE;
-            return launch_tile(t->rpl[r - 1].obs, t->rpl[r - 1].lds, r, L, args, pr, stream,
-                               "marlnav_observe");
         }
     g_last_family = MARLNAV_FAMILY_WAVE;
     return launch(select_kernels(d->num_agents, d->num_obstacles).obs, L, args, pr, stream,

@@ -350,7 +350,10 @@ class Env(object):
 
     @_step_num.setter
     def _step_num(self, value):
-        self.__dict__['_step_num_t'] = self._dev_f32(value, (self.num_parallel,))
+        t = self._dev_f32(value, (self.num_parallel,))
+        if isinstance(value, torch.Tensor) and t.data_ptr() == value.data_ptr():
+            t = t.clone()   # steps update it in place: never the caller's storage
+        self.__dict__['_step_num_t'] = t
         self._configure()
 
     @property
@@ -362,6 +365,8 @@ class Env(object):
         t = torch.as_tensor(value).to(device=self.device, dtype=torch.bool).contiguous()
         if tuple(t.shape) != (self.num_parallel,):
             raise ValueError(f"_terminates must be ({self.num_parallel},)")
+        if isinstance(value, torch.Tensor) and t.data_ptr() == value.data_ptr():
+            t = t.clone()
         self.__dict__['_terminates_t'] = t
         self._configure()
 
@@ -463,8 +468,9 @@ class Env(object):
         self._sync_params()
         out = self._new_obs()
         abi.check(self._lib.marlnav_observe(
-            ctypes.byref(self._dims), self._states.data_ptr(), self._obstacles.data_ptr(),
-            self._target.data_ptr(), out.data_ptr(), _stream_handle(self.device)), self._lib)
+            ctypes.byref(self._dims), ctypes.byref(self._cparams), self._states.data_ptr(),
+            self._obstacles.data_ptr(), self._target.data_ptr(), out.data_ptr(),
+            _stream_handle(self.device)), self._lib)
         return self._wrap_obs(out)
 
     def _coerce_actions(self, actions):
@@ -472,6 +478,8 @@ class Env(object):
         if actions.shape[-1] != 2:
             actions = actions[..., [0, -1]]  # angle = [..., 0], accel = [..., -1]
         actions = actions.to(device=self.device, dtype=_F32).contiguous()
+        if actions.data_ptr() % 16:
+            actions = actions.clone()   # a view at an odd offset: the compiled kernels stage 16-B pieces
         if tuple(actions.shape) != self._act_shape:
             raise ValueError(f"actions must be {self._act_shape}, got {tuple(actions.shape)}")
         return actions
@@ -485,6 +493,9 @@ class Env(object):
         (An Env instance's ``step`` attribute is the native host engine; this
         method is what it runs for calls its fast path does not take.)"""
         return self._engine(actions)
+
+    def _blend_kept(self, out, fresh):
+        _blend_kept_impl(self, out, fresh)
 
     @property
     def _step_idx(self):
@@ -500,7 +511,8 @@ class Env(object):
         dev = self.device
         if not (type(actions) is torch.Tensor and actions.dtype is _F32
                 and actions.device == dev and actions.shape == self._act_shape
-                and actions.is_contiguous() and not actions.requires_grad):
+                and actions.is_contiguous() and not actions.requires_grad
+                and actions.data_ptr() % 16 == 0):
             actions = self._coerce_actions(actions)
         eng = self._engine
         if self._rng == 'native' and self._init_sampler is self._default_init_sampler:
@@ -512,8 +524,15 @@ class Env(object):
         S = self._obstacles.shape[1]
         keep = (self._dev_f32(fs, (P, self.num_agents, 5)),
                 self._dev_f32(fo, (P, S, 2)), self._dev_f32(ft, (P, 1, 2)))
+        # the reference blends every env with its fresh candidate
+        # (environment.py:86-90): a non-finite candidate turns even a kept
+        # env's value into NaN (0 * inf). The kernel reads candidates of
+        # finished envs only; kept ones are fixed up below in that case.
+        poisoned = not all(bool(torch.isfinite(t).all()) for t in (fs, fo, ft))
         flags = abi.FRESH_STATES_FROM_MOVED if self._mock_alias else 0
         out = eng.launch(actions.data_ptr(), tuple(t.data_ptr() for t in keep), flags)
+        if poisoned:
+            self._blend_kept(out, keep)
         if self._mock_alias:
             # the reference's MockInitializer now holds the post-move states
             # (utils.py:310-319 aliasing); later re-inits restore them
@@ -523,6 +542,29 @@ class Env(object):
                 init.states = self._states.clone()
         del keep   # stream-ordered: the caching allocator reuses them after the kernel
         return out
+
+
+def _blend_kept_impl(env, out, fresh):
+    """Kept envs (mask 0) of a step whose fresh candidates hold non-finite
+    values: old + 0 * fresh (environment.py:86-90), then the step's
+    observations (and the fused normaliser's copy) of the blended state,
+    which for finished envs equal what the kernel wrote."""
+    obs, rew, term, trunc = out
+    kept = ~torch.logical_or(term, trunc)
+    fs, fo, ft = fresh
+    if env._mock_alias:
+        fs = env._states.clone()   # the aliased mock holds the moved states
+    for buf, f in ((env._states, fs), (env._obstacles, fo), (env._target, ft)):
+        m = kept.view(-1, *([1] * (buf.dim() - 1)))
+        buf.copy_(torch.where(m, buf + 0.0 * f, buf))
+    packed = obs._packed
+    abi.check(env._lib.marlnav_observe(
+        ctypes.byref(env._dims), ctypes.byref(env._cparams), env._states.data_ptr(),
+        env._obstacles.data_ptr(), env._target.data_ptr(), packed.data_ptr(),
+        _stream_handle(env.device)), env._lib)
+    if obs._normalized is not None:
+        mean, scale = env._obs_norm_buffers
+        torch.div(packed - mean, scale, out=obs._normalized)
 
 
 def _new_output_set(env):

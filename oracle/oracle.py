@@ -36,7 +36,7 @@ def load():
         lib.oracle_step.argtypes = [dims_p, par_p, ctypes.POINTER(_abi.MarlnavStepBuffers),
                                     ctypes.c_uint64, ctypes.c_int64]
         lib.oracle_step.restype = None
-        lib.oracle_observe.argtypes = [dims_p, P, P, P, P]
+        lib.oracle_observe.argtypes = [dims_p, par_p, P, P, P, P]
         lib.oracle_observe.restype = None
         lib.oracle_reinit_all.argtypes = [dims_p, par_p, P, P, P, P, ctypes.c_uint64]
         lib.oracle_reinit_all.restype = None
@@ -77,11 +77,17 @@ def obs_dim(A, O):
     return 2 + 2 * O + 2 * (A - 1)
 
 
-def observe(dims, states, obstacles, target):
+def observe(dims, states, obstacles, target, params=None):
+    """observations() (environment.py:139-180); params supplies the angle
+    cap (cap_distance; the reference's 0.1 when params is None)."""
     P, A, O = dims.num_parallel, dims.num_agents, dims.num_obstacles
     st, ob, tg = _f32(states), _f32(obstacles), _f32(target)
     out = np.empty((P, A, obs_dim(A, O)), np.float32)
-    load().oracle_observe(ctypes.byref(dims), _ptr(st), _ptr(ob), _ptr(tg), _ptr(out))
+    if params is None:
+        params = _abi.MarlnavParams()
+        params.cap_distance = 0.1
+    load().oracle_observe(ctypes.byref(dims), ctypes.byref(params), _ptr(st), _ptr(ob),
+                          _ptr(tg), _ptr(out))
     return out
 
 

@@ -188,3 +188,70 @@ def test_oracle_process_rewards_matches_reference():
         assert abs(mean - float(z[f"case{k}_mean"])) <= 1e-12 * max(1.0, abs(mean))
         k += 1
     assert k == 3
+
+
+@pytest.mark.parametrize("A,O", [(3, 3), (3, 8), (5, 2)])
+def test_oracle_blend_matches_reference_expression_on_non_finite_values(A, O, mk):
+    """The re-init blend (environment.py:86-90) on values no golden vector
+    holds: NaN/inf old states of finished envs, NaN/inf fresh candidates of
+    kept envs. The oracle against oracle/torch_ref.py, which evaluates the
+    reference's own expression (einsum of the int64 mask, pinned bit for bit
+    to the reference goldens in tests/test_torch_ref.py): NaN positions,
+    infinities and finite values equal."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "oracle"))
+    from torch_ref import TorchRefEnv
+    P = 24
+    g = torch.Generator().manual_seed(A * 10 + O)
+    ref = TorchRefEnv(P, A, O, episode_len=3, factors=dict(risk=2.0, distance=3.0))
+    st = ref.states.clone()
+    st[:, :, :2] += torch.rand(P, A, 2, generator=g) * 40.0
+    ob = ref.obstacles.clone()
+    tg = ref.target.clone()
+    sn = torch.zeros(P)
+    sn[::2] = 2.0                                    # even envs truncate this step
+    nan, inf = float("nan"), float("inf")
+    st[0, 0, 0] = nan                                # finished env, NaN old position
+    st[2, 1, 2] = inf                                # finished env, inf old heading
+    ob[4, O - 1, 1] = nan                            # finished env, NaN old obstacle
+    tg[6, 0, 0] = -inf                               # finished env, -inf old target
+    fs = torch.rand(P, A, 5, generator=g) * 900.0
+    fo = torch.rand(P, O, 2, generator=g) * 700.0
+    ft = torch.rand(P, 1, 2, generator=g) * 1400.0
+    fs[1, 0, 3] = nan                                # kept env, NaN candidate
+    fo[3, 0, 0] = inf                                # kept env, inf candidate
+    ft[5, 0, 1] = -inf
+    fs[8, 2 % A, 0] = inf                            # finished env, inf candidate
+    acts = (torch.rand(P, A, 2, generator=g) - 0.5) * 0.5
+    ref.states, ref.obstacles, ref.target = st.clone(), ob.clone(), tg.clone()
+    ref.step_num = sn.clone()
+    ref.fresh_override = lambda: (fs.clone(), fo.clone(), ft.clone())
+    r_obs, r_rew, r_term, r_trunc = ref.step(acts.clone())
+    pr = mk({"min_speed": 3.0, "max_speed": 10.0, "min_accel": -0.5, "max_accel": 0.5,
+             "_risk_factor": 2.0, "_distance_factor": 3.0, "_heading_factor": 500.0,
+             "_target_factor": 500.0, "_soft_factor": 500.0, "_bond_factor": 10.0,
+             "episode_len": 3})
+    dm = orc.make_dims(P, A, O)
+    o = orc.step(dm, pr, st.numpy(), ob.numpy(), tg.numpy(), sn.numpy(),
+                 np.zeros(P, np.bool_), acts.numpy(),
+                 fresh=(fs.numpy(), fo.numpy(), ft.numpy()))
+    np.testing.assert_array_equal(o["truncated"], r_trunc.numpy())
+    np.testing.assert_array_equal(o["terminated"], r_term.numpy())
+    # sin/cos of the heading: torch's SLEEF vs the oracle's correctly rounded
+    # value (<= 1 ulp), hence states/rewards within tolerance, NaN for NaN
+    assert_states_close(o["states"], ref.states.numpy(), "states")
+    assert_vec_close(o["reward"], r_rew.numpy(), what="reward")
+    for name, want in (("obstacles", ref.obstacles), ("target", ref.target),
+                       ("step_num", ref.step_num)):
+        np.testing.assert_array_equal(o[name], want.numpy(), name)
+    # observations: NaN / inf positions equal; finite values within what the
+    # states' 1-ulp heading differences can move them (acos is
+    # ill-conditioned next to 0, so angles get an absolute 1e-4 there)
+    for f, a, e in zip(OBS_FIELDS, orc.split_obs(o["obs"], A, O), r_obs):
+        assert_vec_close(a, e.numpy(), rtol=1e-4, atol=1e-4 if "angle" in f else 0.0,
+                         what="blend " + f)
+    # the cases above really are exercised: NaN where the reference has NaN
+    assert np.isnan(o["states"][0, 0, 0]) and np.isnan(o["states"][1, 0, 3])
+    assert np.isnan(o["obstacles"][3, 0, 0]) and o["states"][8, 2 % A, 0] == inf
