@@ -1,0 +1,849 @@
+// device_math.h - device arithmetic of the step: exact fp32 pair math (cdist / normalize / acos as the reference evaluates them), heading sin/cos, Philox re-init draws, torch-order row sums, the per-row observation, LDS plans.
+// Part of libmarlnav.so: included once, by marlnav_step.hip (one translation
+// unit), inside its anonymous namespace.
+#pragma once
+
+__host__ __device__ inline int obs_dim(int A, int O) { return 2 + 2 * O + 2 * (A - 1); }
+
+// ------------------------------------------------------------- device math
+__device__ __forceinline__ float clamp_t(float x, float lo, float hi)
+{
+    x = x < lo ? lo : x;  // NaN passes through like torch.clamp
+    return x > hi ? hi : x;
+}
+
+// Observation rows and states of the env-block and pair-split kernels leave
+// through streaming stores (`nt`): nothing in the launch reads them back, and
+// dirty lines kept in the XCD's L2 only lengthen the end-of-launch
+// write-back. Measured: 65536x3x3 10.3 -> 9.4 us, 65536x3x8 13.0 -> 11.5 us,
+// 2^21 envs 150 -> 144 us, 4096x16x32 18.0 -> 17.3 us. Per-env scalars (one
+// env per wave in the split kernel: 1-4 byte stores) measured slower with nt
+// and stay plain, as do the wave kernel's stores.
+constexpr bool kNtRows = true;    // rows and states of the block/split kernels
+constexpr bool kNtOther = false;  // per-env scalars and the wave kernel
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+
+template <bool NT = kNtOther, class T>
+__device__ __forceinline__ void out_st(T *p, T v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <bool NT = kNtOther>
+__device__ __forceinline__ void out_st4(float *p, float4 v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v4f_t{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f_t *>(p));
+    else
+        *reinterpret_cast<float4 *>(p) = v;
+}
+
+template <bool NT = kNtOther>
+__device__ __forceinline__ void out_st2(float *p, float2 v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v2f_t{v.x, v.y}, reinterpret_cast<v2f_t *>(p));
+    else
+        *reinterpret_cast<float2 *>(p) = v;
+}
+
+// Fast-path switches for the pair math in FAST mode: 1 = the shortened
+// sequence (bit-exact inside its guard, scripts/probes/fastmath_probe.hip),
+// 0 = the IEEE operation. The tile kernels enter FAST mode only for a wave
+// whose every coordinate passed coords_in_range() (which implies every
+// per-pair guard), so there the guards are dead code. Kernels that evaluate
+// the guards per pair (wave/split kernels) were measured slower with them and
+// run IEEE-only (kGuardedFast).
+constexpr bool kGuardedFast = false;
+// Internal MarlnavParams.flags bit set by marlnav_step when every reward
+// parameter lies inside the short division sequences' guards
+// (terms_fast_params): the observe_row_own reward terms then use them in
+// FAST (coordinate-checked) waves. Never set by callers (above the public
+// MARLNAV_* flag bits).
+constexpr uint32_t kTermsFastFlag = 1u << 30;
+
+// x == 0 or x = m * 2^e with e in [-59, 62] (|x| in [2^-60, 2^62)); NaN and
+// infinities pass (they also fail the denominators' guard)
+__device__ __forceinline__ bool exp_ok(float x)
+{
+    return (unsigned)(__builtin_amdgcn_frexp_expf(x) + 59) <= 121u;
+}
+
+// |x| in [lo, hi] or x == 0
+__device__ __forceinline__ bool mag_ok(float x, float lo, float hi)
+{
+    const float ax = fabsf(x);
+    return (ax >= lo && ax <= hi) || x == 0.0f;
+}
+
+// A coordinate the fast pair math accepts without per-pair guards: zero or
+// |c| in [2^-20, 2^40]. If every position a row uses satisfies it, every
+// nonzero difference is >= 2^-43 and <= 2^41, so each pair's squared
+// distance lies in [2^-86, 2^83] (sqrt_fast guard [2^-96, 2^96]), each
+// distance in [1e-12 clamp, 2^42] and each numerator zero or in
+// [2^-43, 2^41] (div2_fast guard [2^-60, 2^60]).
+__device__ __forceinline__ bool coord_ok(float c) { return mag_ok(c, 0x1p-20f, 0x1p40f); }
+
+// coord_ok over many values without per-value compares: |c| as bits is
+// monotone for non-negative floats, so accumulate min(bits - 1) (0 wraps to
+// the largest value: zero passes) and max(bits) (NaN and inf exceed 2^40),
+// then compare once. Equal to AND over coord_ok.
+struct CoordRange {
+    uint32_t lo = 0xffffffffu, hi = 0u;
+    __device__ void add(float c)
+    {
+        const uint32_t u = __float_as_uint(c) & 0x7fffffffu;
+        lo = u - 1u < lo ? u - 1u : lo;
+        hi = u > hi ? u : hi;
+    }
+    __device__ bool ok() const
+    {
+        return lo >= __float_as_uint(0x1p-20f) - 1u && hi <= __float_as_uint(0x1p40f);
+    }
+};
+
+// coord_ok over a full tile's staged obstacle (NOB floats) and target (NTG)
+// coordinates, spread over the wave's lanes
+template <int NOB, int NTG>
+__device__ __forceinline__ bool tile_coords_ok(const float *ob, const float *tg, unsigned lane)
+{
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k * 64 < NOB; ++k) {
+        const int i = k * 64 + (int)lane;
+        if ((k + 1) * 64 <= NOB || i < NOB) ok = ok && coord_ok(ob[i]);
+    }
+#pragma unroll
+    for (int k = 0; k * 64 < NTG; ++k) {
+        const int i = k * 64 + (int)lane;
+        if ((k + 1) * 64 <= NTG || i < NTG) ok = ok && coord_ok(tg[i]);
+    }
+    return ok;
+}
+
+// Correctly rounded sqrt for x in [2^-96, 2^96] or x == 0: hipcc's own
+// IEEE sequence (v_sqrt_f32, then the neighbour whose residual straddles x)
+// without its input scaling and special-value class fix-up, which only act
+// outside that range; `ok` is cleared outside it (the caller redoes the row
+// with the full sequence).
+__device__ __forceinline__ float sqrt_fast(float x, bool &ok)
+{
+    ok &= (x >= 0x1p-96f && x <= 0x1p96f) || x == 0.0f;
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float s_dn = __int_as_float(__float_as_int(s) - 1);
+    const float s_up = __int_as_float(__float_as_int(s) + 1);
+    // x - s_dn*s with the sign on the float operand (a free source modifier;
+    // negating the integer-built neighbour costs a v_xor per pair)
+    const float r_dn = __builtin_fmaf(s_dn, -s, x);
+    const float r_up = __builtin_fmaf(s_up, -s, x);
+    s = r_dn <= 0.0f ? s_dn : s;
+    return r_up > 0.0f ? s_up : s;
+}
+
+// torch.cdist direct path (environment.py:271-274)
+template <bool FAST = false>
+__device__ __forceinline__ float pair_dist(float ox, float oy, float px, float py, bool &ok)
+{
+    const float dx = px - ox, dy = py - oy;
+    if constexpr (FAST)
+        return sqrt_fast(__builtin_fmaf(dy, dy, dx * dx), ok);
+    else
+        return __builtin_sqrtf(__builtin_fmaf(dy, dy, dx * dx));
+}
+
+__device__ __forceinline__ float pair_dist(float ox, float oy, float px, float py)
+{
+    bool ok = true;
+    return pair_dist<false>(ox, oy, px, py, ok);
+}
+
+// Division by a wave-uniform constant c (a reward parameter): the same
+// core sequence as div2_fast with the reciprocal refined once per use site
+// (uniform, so once per wave). Guard: c in [2^-20, 2^20], the numerator zero
+// or in [2^-70, 2^70], so every intermediate stays normal; `ok` cleared
+// otherwise.
+struct DivC {
+    float c, r;
+};
+
+__device__ __forceinline__ DivC make_divc(float c, bool &ok)
+{
+    const float ac = fabsf(c);
+    ok &= ac >= 0x1p-20f && ac <= 0x1p20f;
+    float r = __builtin_amdgcn_rcpf(c);
+    r = __builtin_fmaf(__builtin_fmaf(-c, r, 1.0f), r, r);
+    return DivC{c, r};
+}
+
+__device__ __forceinline__ float div_c(float x, DivC d, bool &ok)
+{
+    ok &= mag_ok(x, 0x1p-70f, 0x1p70f);
+    float q = x * d.r;
+    q = __builtin_fmaf(__builtin_fmaf(-d.c, q, x), d.r, q);
+    return __builtin_fmaf(__builtin_fmaf(-d.c, q, x), d.r, q);
+}
+
+// 1 / den for den in [1, 2^96] (the bond term's 1 + sd^2): div2_fast's core.
+__device__ __forceinline__ float recip_fast(float den, bool &ok)
+{
+    ok &= den <= 0x1p96f;
+    float r = __builtin_amdgcn_rcpf(den);
+    r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    const float q = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    return __builtin_fmaf(__builtin_fmaf(-den, q, 1.0f), r, q);
+}
+
+// Two correctly rounded quotients over one denominator. This is hipcc's own
+// IEEE fp32 division sequence (reciprocal refined by one Newton step, two
+// residual corrections) with the v_div_scale / v_div_fixup range steps
+// dropped and the reciprocal shared. Those steps only matter when a quotient,
+// reciprocal or residual leaves the normal range; the guard keeps every
+// intermediate normal: den in [2^-60, 2^60] (den is a pair distance clamped
+// at 1e-12, so |x|, |y| <= den) and numerators zero or >= 2^-60 in magnitude.
+// `ok` is cleared otherwise and the caller redoes the row with IEEE division.
+// Branch-free, so consecutive pairs interleave. Checked bit-exact against
+// IEEE division on the GPU: scripts/probes/fastmath_probe.hip.
+__device__ __forceinline__ void div2_fast(float x, float y, float den, float *qx, float *qy,
+                                          bool &ok)
+{
+    ok &= den >= 0x1p-60f && den <= 0x1p60f && mag_ok(x, 0x1p-60f, 0x1p60f) &&
+          mag_ok(y, 0x1p-60f, 0x1p60f);
+    float r = __builtin_amdgcn_rcpf(den);
+    r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
+    float q = x * r;
+    q = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
+    *qx = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
+    q = y * r;
+    q = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
+    *qy = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
+}
+
+// _get_angles (environment.py:276-286) + the dist < 0.1 cap (:172-177).
+// FAST: shared-reciprocal division (clears ok when it may differ from IEEE).
+template <bool FAST = false>
+__device__ __forceinline__ float pair_angle(float ox, float oy, float px, float py,
+                                            float dirx, float diry, float dist, float cap,
+                                            bool &ok)
+{
+    const float dx = px - ox, dy = py - oy;
+    // F.normalize's clamp_min(1e-12). FAST (finite, non-negative dist): one
+    // v_med3 instead of a canonicalize + v_max
+    const float den = FAST ? __builtin_amdgcn_fmed3f(dist, 1e-12f, __builtin_inff())
+                           : (dist > 1e-12f ? dist : 1e-12f);
+    float nx, ny;
+    if constexpr (FAST) {
+        div2_fast(dx, dy, den, &nx, &ny, ok);
+    } else {
+        nx = dx / den;
+        ny = dy / den;
+    }
+    float dot = dirx * nx + diry * ny;
+    // FAST: dot is finite, so the clamp is one v_med3 (no compare/select
+    // pairs and their VCC hazard nops); -0 passes through either way
+    dot = FAST ? __builtin_amdgcn_fmed3f(dot, -1.0f, 1.0f) : clamp_t(dot, -1.0f, 1.0f);
+    const float orth_x = nx - dot * dirx;
+    const float ang = (orth_x > 0.0f ? -1.0f : 1.0f) * acosf(dot);
+    return dist < cap ? 0.0f : ang;
+}
+
+// sin/cos of an angle already clamped to [-pi, pi], evaluated in double and
+// rounded once: Cody-Waite reduction by pi/2 (two-part constant, |k| <= 2)
+// and the fdlibm __kernel_sin/__kernel_cos minimax polynomials on
+// [-pi/4, pi/4]. Identical expression tree in oracle/marlnav_oracle.c.
+__device__ __forceinline__ void sincos_k(float th, float *s_out, float *c_out)
+{
+    const double x = (double)th;
+    const double k = __builtin_rint(x * 6.36619772367581382433e-01);
+    double r = __builtin_fma(-k, 1.57079632679489655800e+00, x);
+    r = __builtin_fma(-k, 6.12323399573676603587e-17, r);
+    r = k == 0.0 ? x : r;  // keeps the sign of -0
+    const double z = r * r;
+    double ps = __builtin_fma(1.58969099521155010221e-10, z, -2.50507602534068634195e-08);
+    ps = __builtin_fma(ps, z, 2.75573137070700676789e-06);
+    ps = __builtin_fma(ps, z, -1.98412698298579493134e-04);
+    ps = __builtin_fma(ps, z, 8.33333333332248946124e-03);
+    ps = __builtin_fma(ps, z, -1.66666666666666324348e-01);
+    const double sn = r == 0.0 ? r : __builtin_fma(r * z, ps, r);  // sin(-0) = -0
+    double pc = __builtin_fma(-1.13596475577881948265e-11, z, 2.08757232129817482790e-09);
+    pc = __builtin_fma(pc, z, -2.75573143513906633035e-07);
+    pc = __builtin_fma(pc, z, 2.48015872894767294178e-05);
+    pc = __builtin_fma(pc, z, -1.38888888888741095749e-03);
+    pc = __builtin_fma(pc, z, 4.16666666666666019037e-02);
+    const double cs = __builtin_fma(z * z, pc, __builtin_fma(-0.5, z, 1.0));
+    const int q = ((int)k) & 3;
+    const double s = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
+    const double c = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
+    *s_out = (float)s;
+    *c_out = (float)c;
+}
+
+// ----------------------------------------------------------- native RNG
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        // one v_mad_u64_u32 per product instead of v_mul_lo_u32 + v_mul_hi_u32
+        const uint64_t p0 = (uint64_t)c[0] * 0xD2511F53u, p1 = (uint64_t)c[2] * 0xCD9E8D57u;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+// uniform #idx of env gid at step s, in [0, 1) on a 24-bit grid
+__device__ __forceinline__ float native_uniform(uint64_t seed, uint64_t gid, uint64_t s,
+                                                uint32_t idx)
+{
+    uint32_t c[4] = {idx >> 2, (uint32_t)s, (uint32_t)gid,
+                     (uint32_t)(gid >> 32) ^ ((uint32_t)(s >> 32) << 16)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t r = c[idx & 3u];
+    return (float)(r >> 8) * 0x1.0p-24f;
+}
+
+// _reinit_update (environment.py:86-90) for a finished env (mask 1):
+// 0*old + 1*fresh, so a non-finite old value stays NaN. Idempotent in the
+// old value (blend(blend(x, f), f) has blend(x, f)'s value), so readers that
+// race with an in-place blend of the same element get the same number.
+__device__ __forceinline__ float blend_in(float old, float fresh) { return 0.0f * old + fresh; }
+
+// native TriangleIntitializer draw for one env (utils.py:375-398); BLEND:
+// blended into the env's current values (a re-init), else written (the
+// initial state)
+template <bool NOISY, bool BLEND = true>
+__device__ void native_fresh_env(int A, int S, const MarlnavParams &pr,
+                                 const float *__restrict__ formation, uint64_t gid,
+                                 uint64_t sidx, float *st, float *ob, float *tg)
+{
+    const auto put = [](float *d, float v) { *d = BLEND ? blend_in(*d, v) : v; };
+    for (int j = 0; j < S; j += 2) {  // one Philox block = 2 obstacles
+        uint32_t c[4] = {(uint32_t)(j >> 1), (uint32_t)sidx, (uint32_t)gid,
+                         (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
+        philox4x32_10(c, (uint32_t)pr.seed, (uint32_t)(pr.seed >> 32));
+        put(ob + 2 * j, pr.obs_range_x * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x);
+        put(ob + 2 * j + 1, pr.obs_range_y * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y);
+        if (j + 1 < S) {
+            put(ob + 2 * j + 2, pr.obs_range_x * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x);
+            put(ob + 2 * j + 3, pr.obs_range_y * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y);
+        }
+    }
+    put(tg, formation[5 * A]);
+    put(tg + 1, formation[5 * A + 1]);
+    for (int i = 0; i < A; ++i) {
+        float f[5];
+        for (int k = 0; k < 5; ++k) f[k] = formation[5 * i + k];
+        if (NOISY) {
+            const uint32_t base = (uint32_t)(2 * S);
+            const float u1 = native_uniform(pr.seed, gid, sidx, base + 3 * i);
+            const float u2 = native_uniform(pr.seed, gid, sidx, base + 3 * i + 1);
+            const float u3 = native_uniform(pr.seed, gid, sidx, base + 3 * i + 2);
+            const double rad = sqrt(-2.0 * log(1.0 - (double)u1));
+            const double ang = 6.283185307179586 * (double)u2;
+            const float z0 = (float)(rad * cos(ang)), z1 = (float)(rad * sin(ang));
+            f[0] = f[0] + pr.ags_dist * (pr.noise_std * z0);
+            f[1] = f[1] + pr.ags_dist * (pr.noise_std * z1);
+            float sn, c;
+            sincos_k(pr.angle_range * (u3 - 0.5f), &sn, &c);
+            const float dx = f[2], dy = f[3];
+            f[2] = c * dx + (-sn) * dy;
+            f[3] = sn * dx + c * dy;
+        }
+        for (int k = 0; k < 5; ++k) put(st + 5 * i + k, f[k]);
+    }
+}
+
+// torch's CPU float summation order over a contiguous row of n values
+// (cascade_sum, aten/src/ATen/native/cpu/SumKernel.cpp; restated and pinned
+// in oracle/marlnav_oracle.c: torch_row_sum). f maps each stored value.
+template <typename F>
+__device__ __forceinline__ float torch_row_sum(const float *x, int n, F f)
+{
+    if (n >= 8) {
+        const int V = n >> 3, m = V >> 2;
+        float acc[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[k][l] = 0.0f;
+        for (int r = 0; r < m; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = 0; l < 8; ++l) acc[k][l] += f(x[(4 * r + k) * 8 + l]);
+        for (int v = 4 * m; v < V; ++v)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[0][l] += f(x[v * 8 + l]);
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[0][l] += acc[k][l];
+        float fin = 0.0f;
+        for (int i = 8 * V; i < n; ++i) fin += f(x[i]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) fin += acc[0][l];
+        return fin;
+    }
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    const int m = n >> 2;
+    for (int r = 0; r < m; ++r) {
+        a0 += f(x[4 * r]);
+        a1 += f(x[4 * r + 1]);
+        a2 += f(x[4 * r + 2]);
+        a3 += f(x[4 * r + 3]);
+    }
+    for (int i = 4 * m; i < n; ++i) a0 += f(x[i]);
+    a0 += a1;
+    a0 += a2;
+    a0 += a3;
+    return a0;
+}
+
+// Make LDS writes of some lanes visible to later LDS reads of other lanes of
+// the SAME wave: the LDS executes one wave's requests in issue order, so only
+// the compiler must be kept from reordering across this point.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ------------------------------------------------------------ wave staging
+// Copy three contiguous global ranges into the wave's LDS slice with every
+// global load issued before the first wait (a load -> LDS-store -> load loop
+// would pay one memory round trip per iteration).
+struct Span {
+    const float *src;
+    float *dst;
+    int n;  // floats
+};
+
+__device__ __forceinline__ const float *span_src(const Span &a, const Span &b, const Span &c,
+                                                 int i, int na, int nb)
+{
+    return i < na ? a.src + i : (i < na + nb ? b.src + (i - na) : c.src + (i - na - nb));
+}
+
+__device__ __forceinline__ float *span_dst(const Span &a, const Span &b, const Span &c, int i,
+                                           int na, int nb)
+{
+    return i < na ? a.dst + i : (i < na + nb ? b.dst + (i - na) : c.dst + (i - na - nb));
+}
+
+// Load span x as 16-byte vectors, K per lane, branch-free: lanes past the end
+// re-read the span's first vector (or, for a span shorter than one vector,
+// the first vector of `safe`), so every load is in bounds and the loads issue
+// back to back; the wait lands at the first LDS write.
+template <int K>
+__device__ __forceinline__ void load_vecs(const Span &x, const float *safe, int lane, float4 (&r)[K])
+{
+    const int n4 = x.n >> 2;
+    const float4 *src = reinterpret_cast<const float4 *>(n4 > 0 ? x.src : safe);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = lane + 64 * k;
+        r[k] = src[i < n4 ? i : 0];
+    }
+}
+
+// Keep the compiler from sinking the loads of r next to their LDS stores:
+// the values must be in VGPRs here, after every load of the tile was issued.
+template <int K>
+__device__ __forceinline__ void pin_vecs(float4 (&r)[K])
+{
+#pragma unroll
+    for (int k = 0; k < K; ++k) asm volatile("" : "+v"(r[k].x), "+v"(r[k].y), "+v"(r[k].z), "+v"(r[k].w));
+}
+
+template <int K>
+__device__ __forceinline__ void store_vecs(const Span &x, int lane, const float4 (&r)[K])
+{
+    const int n4 = x.n >> 2;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = lane + 64 * k;
+        if (i < n4) reinterpret_cast<float4 *>(x.dst)[i] = r[k];
+    }
+    for (int i = lane + 64 * K; i < n4; i += 64)  // spans longer than K vectors per lane
+        reinterpret_cast<float4 *>(x.dst)[i] = reinterpret_cast<const float4 *>(x.src)[i];
+}
+
+// Stage three spans into the wave's LDS slice. KA/KB/KC: vectors per lane
+// loaded ahead for each span (exact for compile-time tile shapes).
+template <int KA, int KB, int KC, bool ALIGNED>
+__device__ __forceinline__ void stage_spans(Span a, Span b, Span c, int lane)
+{
+    const bool vec = ALIGNED || (((reinterpret_cast<uintptr_t>(a.src) |
+                                   reinterpret_cast<uintptr_t>(b.src) |
+                                   reinterpret_cast<uintptr_t>(c.src)) & 15u) == 0 && a.n >= 4);
+    if (!vec) {  // unaligned tile base (only W < 4 tiles): plain copy
+        const int nt = a.n + b.n + c.n;
+        for (int i = lane; i < nt; i += 64)
+            *span_dst(a, b, c, i, a.n, b.n) = *span_src(a, b, c, i, a.n, b.n);
+        return;
+    }
+    float4 ra[KA], rb[KB], rc[KC];
+    load_vecs<KA>(a, a.src, lane, ra);
+    load_vecs<KB>(b, a.src, lane, rb);
+    load_vecs<KC>(c, a.src, lane, rc);
+    // scalar tails (< 4 floats per span, partial last tile only): lanes 0..11
+    const int tw = lane >> 2, tj = lane & 3;
+    const Span &tsp = tw == 0 ? a : (tw == 1 ? b : c);
+    const bool has_tail = lane < 12 && tj < (tsp.n & 3);
+    const int toff = (tsp.n & ~3) + tj;
+    float t = has_tail ? tsp.src[toff] : 0.0f;
+    pin_vecs<KA>(ra);
+    pin_vecs<KB>(rb);
+    pin_vecs<KC>(rc);
+    asm volatile("" : "+v"(t));
+    store_vecs<KA>(a, lane, ra);
+    store_vecs<KB>(b, lane, rb);
+    store_vecs<KC>(c, lane, rc);
+    if (has_tail) tsp.dst[toff] = t;
+}
+
+// Stream n floats of the wave's LDS slice to global memory (16-byte stores
+// when the destination allows), optionally also the ObsNormalizer output
+// (utils.py:530-532) of every element.
+__device__ __forceinline__ void wave_store(float *__restrict__ dst, const float *__restrict__ src,
+                                           int n, int lane, float *__restrict__ nrm_dst,
+                                           const float *__restrict__ mean,
+                                           const float *__restrict__ scale, int D)
+{
+    int head = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+        const int n4 = n >> 2;
+        for (int i = lane; i < n4; i += 64)
+            out_st4(dst + 4 * i, *reinterpret_cast<const float4 *>(src + 4 * i));
+        head = n4 << 2;
+    }
+    for (int i = head + lane; i < n; i += 64) out_st(dst + i, src[i]);
+    if (nrm_dst) {
+        for (int i = lane; i < n; i += 64) {
+            const int k = i % D;
+            nrm_dst[i] = (src[i] - mean[k]) / scale[k];
+        }
+    }
+}
+
+// ------------------------------------------------------------ row observe
+struct RowOut {
+    float r_miss, r_hit;  // agent reward if the env misses / reaches the target
+    unsigned flags;       // bit0: obstacle or agent collision, bit1: in target
+};
+
+// observations() for agent row `a` of one env (environment.py:139-180), with
+// the per-agent reward terms of _rews_and_terms (:184-269) when TERMS.
+// `row` is the packed output row (LDS or global, stride 1).
+template <int A_T, int O_T, bool TERMS>
+__device__ __forceinline__ RowOut observe_row(int Arun, int Orun, const float *__restrict__ sts,
+                                              const float *__restrict__ obe,
+                                              const float *__restrict__ tge, int a,
+                                              float *__restrict__ row, const MarlnavParams &pr)
+{
+    const int A = A_T ? A_T : Arun;
+    const int O = O_T ? O_T : Orun;
+    const float cap = pr.cap_distance;
+    const float ox = sts[5 * a], oy = sts[5 * a + 1];
+    const float dx = sts[5 * a + 2], dy = sts[5 * a + 3];
+
+    const float tx = tge[0], ty = tge[1];
+    const float td = pair_dist(ox, oy, tx, ty);
+    bool ok = true;
+    const float ta = pair_angle(ox, oy, tx, ty, dx, dy, td, cap, ok);
+    row[0] = ta;
+    row[1] = td;
+
+    bool ob_risk = false, ob_col = false;
+#pragma unroll
+    for (int j = 0; j < O; ++j) {
+        const float px = obe[2 * j], py = obe[2 * j + 1];
+        const float d = pair_dist(ox, oy, px, py);
+        row[2 + j] = pair_angle(ox, oy, px, py, dx, dy, d, cap, ok);
+        row[2 + O + j] = d;
+        if (TERMS) {
+            ob_risk |= d < pr.ob_risk_dist;
+            ob_col |= d < pr.ob_coll_dist;
+        }
+    }
+
+    bool ag_risk = false, ag_col = false;
+    float band = 0.0f;
+    float *ang_out = row + 2 + 2 * O;
+    float *dst_out = ang_out + (A - 1);
+    int k = 0;
+#pragma unroll
+    for (int m = 0; m < A; ++m) {
+        if (m == a) continue;
+        const float px = sts[5 * m], py = sts[5 * m + 1];
+        const float d = pair_dist(ox, oy, px, py);
+        ang_out[k] = pair_angle(ox, oy, px, py, dx, dy, d, cap, ok);
+        dst_out[k] = d;
+        ++k;
+        if (TERMS) {
+            ag_risk |= d < pr.ag_risk_dist;
+            ag_col |= d < pr.ag_coll_dist;
+            band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1.0f : 0.0f;
+        }
+    }
+
+    RowOut out{0.0f, 0.0f, 0u};
+    if (TERMS) {
+        const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+        const float dsc = (band < pr.max_at_prop_d ? band : pr.max_at_prop_d) / pr.max_at_prop_d;
+        const float soft = -1.0f * (td / pr.init_dist);
+        // _bond_reward (environment.py:264-269), summed in torch's order over
+        // the others_distances just written to this row
+        const float ideal = pr.ideal_dist, sharp = pr.bond_sharpness;
+        const float bond = torch_row_sum(dst_out, A - 1, [ideal, sharp](float d) {
+            const float sd = (d - ideal) / sharp;
+            return 1.0f / (1.0f + sd * sd);
+        });
+        const float bondm = bond / (float)(A - 1);
+        const float risk = (ob_risk || ag_risk) ? 1.0f : 0.0f;
+        float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
+        float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
+        rm = rm + pr.distance_factor * dsc;
+        rh = rh + pr.distance_factor * dsc;
+        rm = rm + pr.soft_factor * soft;
+        rh = rh + pr.soft_factor * soft;
+        rm = rm + pr.bond_factor * bondm;
+        rh = rh + pr.bond_factor * bondm;
+        rm = rm - pr.risk_factor * risk;
+        rh = rh - pr.risk_factor * risk;
+        out.r_miss = rm;
+        out.r_hit = rh;
+        out.flags = ((ob_col || ag_col) ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u);
+    }
+    return out;
+}
+
+// torch_row_sum over N values held in registers (compile-time indices, so the
+// array stays in VGPRs).
+template <int N, typename F>
+__device__ __forceinline__ float torch_row_sum_r(const float *x, F f)
+{
+    if constexpr (N >= 8) {
+        constexpr int V = N / 8, M = V / 4;
+        float acc[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[k][l] = 0.0f;
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = 0; l < 8; ++l) acc[k][l] += f(x[(4 * r + k) * 8 + l]);
+#pragma unroll
+        for (int v = 4 * M; v < V; ++v)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[0][l] += f(x[v * 8 + l]);
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[0][l] += acc[k][l];
+        float fin = 0.0f;
+#pragma unroll
+        for (int i = 8 * V; i < N; ++i) fin += f(x[i]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) fin += acc[0][l];
+        return fin;
+    } else {
+        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+        constexpr int M = N / 4;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            a0 += f(x[4 * r]);
+            a1 += f(x[4 * r + 1]);
+            a2 += f(x[4 * r + 2]);
+            a3 += f(x[4 * r + 3]);
+        }
+#pragma unroll
+        for (int i = 4 * M; i < N; ++i) a0 += f(x[i]);
+        a0 += a1;
+        a0 += a2;
+        a0 += a3;
+        return a0;
+    }
+}
+
+// observe_row with compile-time shape and the packed row kept in registers
+// (row[D]); others are visited as j = 0..A-2 -> agent j + (j >= a), so
+// every row index is a compile-time constant.
+// The own row (ox, oy, dx, dy) comes in registers; the env's other agents
+// are read from sts.
+template <int A, int O, bool TERMS, bool FAST>
+__device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
+                                                  const float *__restrict__ obe,
+                                                  const float *__restrict__ tge, int a,
+                                                  float ox, float oy, float dx, float dy,
+                                                  float *row, const MarlnavParams &pr, bool &ok)
+{
+    const float cap = pr.cap_distance;
+    const float td = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
+    const float ta = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, td, cap, ok);
+    row[0] = ta;
+    row[1] = td;
+    bool ob_risk = false, ob_col = false;
+#pragma unroll
+    for (int j = 0; j < O; ++j) {
+        const float px = obe[2 * j], py = obe[2 * j + 1];
+        const float d = pair_dist<FAST>(ox, oy, px, py, ok);
+        row[2 + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
+        row[2 + O + j] = d;
+        if (TERMS) {
+            ob_risk |= d < pr.ob_risk_dist;
+            ob_col |= d < pr.ob_coll_dist;
+        }
+    }
+    bool ag_risk = false, ag_col = false;
+    float band = 0.0f;
+#pragma unroll
+    for (int j = 0; j < A - 1; ++j) {
+        const int m = j + (j >= a ? 1 : 0);
+        const float px = sts[5 * m], py = sts[5 * m + 1];
+        const float d = pair_dist<FAST>(ox, oy, px, py, ok);
+        row[2 + 2 * O + j] = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
+        row[2 + 2 * O + (A - 1) + j] = d;
+        if (TERMS) {
+            ag_risk |= d < pr.ag_risk_dist;
+            ag_col |= d < pr.ag_coll_dist;
+            band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1.0f : 0.0f;
+        }
+    }
+    RowOut out{0.0f, 0.0f, 0u};
+    if (TERMS) {
+        const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+        const float ideal = pr.ideal_dist, sharp = pr.bond_sharpness;
+        const float bandc = band < pr.max_at_prop_d ? band : pr.max_at_prop_d;
+        float dsc, soft, bondm;
+        if (FAST && (pr.flags & kTermsFastFlag)) {
+            // exact: the host set kTermsFastFlag only for parameters inside
+            // the div_c / recip_fast guards (terms_fast_params), and FAST
+            // coordinates bound every distance (coord_ok), so every operand
+            // below stays in range
+            const DivC d_mapd = make_divc(pr.max_at_prop_d, ok);
+            const DivC d_init = make_divc(pr.init_dist, ok);
+            const DivC d_sharp = make_divc(sharp, ok);
+            dsc = div_c(bandc, d_mapd, ok);
+            soft = -1.0f * div_c(td, d_init, ok);
+            const float bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [&](float d) {
+                const float sd = div_c(d - ideal, d_sharp, ok);
+                return recip_fast(1.0f + sd * sd, ok);
+            });
+            bondm = bond / (float)(A - 1);  // the bond sum can be tiny: IEEE
+        } else {
+            dsc = bandc / pr.max_at_prop_d;
+            soft = -1.0f * (td / pr.init_dist);
+            const float bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [ideal, sharp](float d) {
+                const float sd = (d - ideal) / sharp;
+                return 1.0f / (1.0f + sd * sd);
+            });
+            bondm = bond / (float)(A - 1);
+        }
+        const float risk = (ob_risk || ag_risk) ? 1.0f : 0.0f;
+        float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
+        float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
+        rm = rm + pr.distance_factor * dsc;
+        rh = rh + pr.distance_factor * dsc;
+        rm = rm + pr.soft_factor * soft;
+        rh = rh + pr.soft_factor * soft;
+        rm = rm + pr.bond_factor * bondm;
+        rh = rh + pr.bond_factor * bondm;
+        rm = rm - pr.risk_factor * risk;
+        rh = rh - pr.risk_factor * risk;
+        out.r_miss = rm;
+        out.r_hit = rh;
+        out.flags = ((ob_col || ag_col) ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u);
+    }
+    return out;
+}
+
+template <int A, int O, bool TERMS, bool FAST>
+__device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts,
+                                                   const float *__restrict__ obe,
+                                                   const float *__restrict__ tge, int a,
+                                                   float *row, const MarlnavParams &pr,
+                                                   bool &ok)
+{
+    return observe_row_own<A, O, TERMS, FAST>(sts, obe, tge, a, sts[5 * a], sts[5 * a + 1],
+                                              sts[5 * a + 2], sts[5 * a + 3], row, pr, ok);
+}
+
+// Store a register row of D floats with the widest aligned vector stores.
+template <int D>
+__device__ __forceinline__ void store_row(float *__restrict__ dst, const float *row)
+{
+    if constexpr (D % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 4)
+            out_st4(dst + k, make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]));
+    } else if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 2) out_st2(dst + k, make_float2(row[k], row[k + 1]));
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) out_st(dst + k, row[k]);
+    }
+}
+
+// -------------------------------------------------------------- LDS plan
+// Per-wave LDS slice, in floats, identical on host and device.
+struct WavePlan {
+    int W, A, O, S, D, obs_lds;
+    int off_st, off_ob, off_tg, off_obs, off_rm, off_rh, off_fl, off_env, floats;
+};
+
+__host__ __device__ inline int align4(int n) { return (n + 3) & ~3; }  // floats -> 16 B
+
+// packed obs rows kept in registers for compile-time shapes up to this D
+constexpr int kRowRegsMaxD = 40;
+
+__host__ __device__ constexpr int static_obs_dim(int A_T, int O_T)
+{
+    return (A_T > 0 && O_T > 0) ? 2 + 2 * O_T + 2 * (A_T - 1) : 0;
+}
+
+__host__ __device__ inline WavePlan make_plan(int W, int A, int O, int S, bool row_regs)
+{
+    WavePlan p;
+    p.W = W;
+    p.A = A;
+    p.O = O;
+    p.S = S;
+    p.D = obs_dim(A, O);
+    p.obs_lds = !row_regs && W * A * p.D <= kObsTileMax;
+    int o = 0;
+    p.off_st = o;  o += align4(W * A * 5);
+    p.off_ob = o;  o += align4(W * S * 2);
+    p.off_tg = o;  o += align4(W * 2);
+    p.off_obs = o; o += p.obs_lds ? align4(W * A * p.D) : 0;
+    p.off_rm = o;  o += 64;
+    p.off_rh = o;  o += 64;
+    p.off_fl = o;  o += 64;
+    p.off_env = o; o += 64;
+    p.floats = o;
+    return p;
+}
+
+struct StepArgs {
+    MarlnavStepBuffers b;
+    int64_t P;
+    int64_t env_offset;
+    int64_t ntiles;
+    int64_t waves;     // waves in the grid (= counter slots)
+    uint64_t step_idx;
+    int W, A, O, S;
+};

@@ -1,0 +1,407 @@
+// kernel_block.h - env-block kernel (one workgroup of A waves per 64 envs: the A3 headline path).
+// Part of libmarlnav.so: included once, by marlnav_step.hip (one translation
+// unit), inside its anonymous namespace.
+#pragma once
+
+// ------------------------------------------------------- env-block kernel
+// One workgroup of A waves per block of E = 64 consecutive envs: lane l of
+// wave w owns agent w of env l. Every lane holds a row (the tile kernels
+// leave 64 - 3*20 = 4 lanes idle at A3), the agent index is wave-uniform, and
+// the per-env phase runs once per block on wave 0 with all 64 lanes busy
+// instead of on 20 of 64 lanes in every wave. Grid shape: at 65536 envs x 3
+// agents, 1024 blocks of 3 waves = 3 waves on every SIMD, where 64/3-env
+// wave tiles give 3277 waves and a fifth of the SIMDs a fourth wave (measured
+// by scripts/kstamps.py: those SIMDs set the kernel's end).
+// Rows are exchanged through LDS between block barriers (5 per step); the
+// packed observation rows are assembled in LDS and streamed out as one
+// contiguous span (a store instruction covers 1 KiB, 8 cache lines, where
+// register-row stores at a 48-byte lane stride touch 24).
+template <int A, int O>
+struct BlockPlan {
+    static constexpr int E = 64, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
+    static constexpr int NT = 64 * A;                      // threads per block
+    static constexpr int ST = 0;                           // (R, 5)
+    static constexpr int ACT = (ST + R * 5 + 3) & ~3;      // (R, 2)
+    static constexpr int OB = (ACT + R * 2 + 3) & ~3;      // (E, O, 2)
+    static constexpr int TG = (OB + E * O * 2 + 3) & ~3;   // (E, 2)
+    static constexpr int SN = (TG + E * 2 + 3) & ~3;       // (E,)
+    static constexpr int TM = (SN + E + 3) & ~3;           // (E,) bytes
+    static constexpr int FORM = (TM + E / 4 + 3) & ~3;     // 5A + 2 (native re-init)
+    static constexpr int RED = (FORM + 5 * A + 2 + 3) & ~3;  // (R, 4) reward terms
+    static constexpr int OBS = RED + 4 * R;                // (R, D) packed rows
+    static constexpr int LIST = (OBS + R * D + 3) & ~3;    // (E,) finished envs
+    static constexpr int FLG = LIST + E;                   // [0] nfin, [1 + w] wave w coords bad
+    static constexpr int LIST2 = (FLG + 1 + A + 3) & ~3;   // (A-1, E) finished envs, waves >= 1
+    static constexpr int FLOATS = (LIST2 + (A - 1) * E + 3) & ~3;
+    static_assert(A >= 2 && A <= 16, "one wave per agent");
+};
+
+// Copy NB bytes of the block's span k into LDS by LDS-DMA from the wave
+// k % A (spans spread over the block's waves).
+template <int NB>
+__device__ __forceinline__ void block_glds(int k, int A, int w, const void *src, float *dst,
+                                           unsigned lane)
+{
+    if (k % A == w) glds_span<NB>(src, dst, lane);
+}
+
+// plain strided copy of n elements by the block's NT threads (partial block)
+template <class T>
+__device__ __forceinline__ void block_copy(const T *__restrict__ src, T *__restrict__ dst, int n,
+                                           int tid, int nt)
+{
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (int i = tid; i < n; i += nt) dst[i] = src[i];
+}
+
+// LDS span -> global span of n floats by the block's threads; 16-byte
+// vectors for the aligned head (both bases 16-byte aligned by construction)
+__device__ __forceinline__ void block_store(float *__restrict__ dst, const float *__restrict__ src,
+                                            int n, int tid, int nt)
+{
+    const int n4 = n >> 2;
+    for (int i = tid; i < n4; i += nt)
+        out_st4<kNtRows>(dst + 4 * i, reinterpret_cast<const float4 *>(src)[i]);
+    for (int i = (n4 << 2) + tid; i < n; i += nt) out_st<kNtRows>(dst + i, src[i]);
+}
+
+// block_store of two full spans with compile-time sizes (16-byte aligned,
+// multiples of 4 floats): every LDS read of both spans issued before the
+// first global store, so the reads' latency is paid once, not per iteration
+template <int N1, int N2, int NT>
+__device__ __forceinline__ void block_store2(float *__restrict__ d1, const float *__restrict__ s1,
+                                             float *__restrict__ d2, const float *__restrict__ s2,
+                                             int tid)
+{
+    static_assert(N1 % 4 == 0 && N2 % 4 == 0, "whole 16-byte pieces");
+    constexpr int Q1 = N1 / 4, Q2 = N2 / 4, K1 = (Q1 + NT - 1) / NT, K2 = (Q2 + NT - 1) / NT;
+    float4 v1[K1], v2[K2];
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+        if ((k + 1) * NT <= Q1 || tid + k * NT < Q1)
+            v1[k] = reinterpret_cast<const float4 *>(s1)[tid + k * NT];
+#pragma unroll
+    for (int k = 0; k < K2; ++k)
+        if ((k + 1) * NT <= Q2 || tid + k * NT < Q2)
+            v2[k] = reinterpret_cast<const float4 *>(s2)[tid + k * NT];
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+        if ((k + 1) * NT <= Q1 || tid + k * NT < Q1) out_st4<kNtRows>(d1 + 4 * (tid + k * NT), v1[k]);
+#pragma unroll
+    for (int k = 0; k < K2; ++k)
+        if ((k + 1) * NT <= Q2 || tid + k * NT < Q2) out_st4<kNtRows>(d2 + 4 * (tid + k * NT), v2[k]);
+}
+
+
+// Phases (one block barrier after each): stage | move + coordinate check
+// (moved states start streaming out) | observe into LDS rows | rows stream
+// out while wave 0 runs the per-env phase | re-init, re-observe and re-store
+// the finished envs only (none in most blocks).
+template <int A, int O, bool OBS_ONLY, bool NOISY>
+__global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
+{
+    using BP = BlockPlan<A, O>;
+    constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
+    (void)k;  // read through kargs_late()
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+#if MARLNAV_STAMPS
+    unsigned long long t_entry;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
+#endif
+    const int tid = (int)threadIdx.x;
+    const unsigned lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // agent of this wave
+    const int64_t blk = blockIdx.x;
+    const int64_t gw = blk * A + w;  // stamps slot
+    KArgsK *K = kargs_late();
+    const int64_t P = K->a.P;
+    // launch_block's grid is exactly ntiles blocks: no exit test, so the
+    // pointer loads below go out in the same round of kernarg loads as P
+    const StepPtrs b = load_ptrs(K);
+    STAMP(0);
+    float *st = lds + BP::ST;
+    const int64_t e0 = blk * E;
+    const int ne = (int)((P - e0) < E ? (P - e0) : E);
+    const bool full = ne == E;
+
+    // ---- stage the block (spans spread over the waves)
+    if (full) {
+        block_glds<R * 20>(0, A, w, b.states + e0 * (A * 5), st, lane);
+        if (!OBS_ONLY) block_glds<R * 8>(1, A, w, b.actions + e0 * (A * 2), lds + BP::ACT, lane);
+        block_glds<E * O * 8>(2, A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
+        block_glds<E * 8>(3, A, w, b.target + e0 * 2, lds + BP::TG, lane);
+        if (!OBS_ONLY) {
+            block_glds<E * 4>(4, A, w, b.step_num + e0, lds + BP::SN, lane);
+            block_glds<E>(5, A, w, b.terminates + e0, lds + BP::TM, lane);
+            if (b.formation)
+                block_glds<(5 * A + 2) * 4>(6, A, w, b.formation, lds + BP::FORM, lane);
+        }
+    } else {
+        const int nr = ne * A;
+        block_copy(b.states + e0 * (A * 5), st, nr * 5, tid, NT);
+        if (!OBS_ONLY) block_copy(b.actions + e0 * (A * 2), lds + BP::ACT, nr * 2, tid, NT);
+        block_copy(b.obstacles + e0 * (O * 2), lds + BP::OB, ne * O * 2, tid, NT);
+        block_copy(b.target + e0 * 2, lds + BP::TG, ne * 2, tid, NT);
+        if (!OBS_ONLY) {
+            block_copy(b.step_num + e0, lds + BP::SN, ne, tid, NT);
+            block_copy(b.terminates + e0, reinterpret_cast<uint8_t *>(lds + BP::TM), ne, tid, NT);
+            if (b.formation) block_copy(b.formation, lds + BP::FORM, 5 * A + 2, tid, NT);
+        }
+    }
+    const MarlnavParams pr = load_params(K);
+    const int l = (int)lane;  // env of this lane within the block
+    const int r = l * A + w;  // row of this lane
+    const bool row_on = l < ne;
+    const int nrow = ne * A;
+    int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
+    if (tid == 0) *bad_word = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+    __syncthreads();
+    STAMP(1);
+
+    // obstacle and target coordinates of the block for the pair-math choice
+    // (below); read before the move writes LDS, so the reads overlap it
+    // (a partial last block takes the IEEE path without checking)
+    CoordRange crange;
+    if (full) {
+        constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
+        static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
+#pragma unroll
+        for (int k2 = 0; k2 * NT < NC; ++k2) {
+            const int i = tid + k2 * NT;
+            if ((k2 + 1) * NT <= NC || i < NC) crange.add(lds[BP::OB + i]);
+        }
+    }
+
+    // ---- _move_agents (environment.py:113-123), own row in registers
+    float ox, oy, dx, dy;
+    {
+        const float *s = st + 5 * r;
+        ox = s[0];
+        oy = s[1];
+        dx = s[2];
+        dy = s[3];
+    }
+    if (!OBS_ONLY) {
+        const float2 act = reinterpret_cast<const float2 *>(lds + BP::ACT)[r];
+        float a0 = act.x, a1 = act.y;
+        if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
+            KArgsK *kl = kargs_late();
+            a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
+            a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
+        }
+        float sn, c;
+        sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+        const float ndx = c * dx + (-sn) * dy;
+        const float ndy = sn * dx + c * dy;
+        float *s = st + 5 * r;
+        const float v = clamp_t(s[4] + clamp_t(a1, pr.min_accel, pr.max_accel), pr.min_speed,
+                                pr.max_speed);
+        ox = ox + ndx * v;
+        oy = oy + ndy * v;
+        dx = ndx;
+        dy = ndy;
+        if (row_on) {
+            s[0] = ox;
+            s[1] = oy;
+            s[2] = dx;
+            s[3] = dy;
+            s[4] = v;
+        }
+    }
+    // block-uniform choice of the pair math: the short sqrt / shared-
+    // reciprocal division (equal to IEEE there) when every coordinate of the
+    // block (obstacles and targets above, moved agents here) passes coord_ok,
+    // IEEE otherwise
+    if (full) {
+        crange.add(ox);
+        crange.add(oy);
+        // one word for the block, written only by waves that found one (all
+        // write 1: a benign race); read once after the barrier
+        const bool bad = __ballot(!crange.ok()) != 0ull;
+        if (lane == 0 && bad) *bad_word = 1;
+    }
+    __syncthreads();
+    STAMP(2);
+    // the moved states are final except in finished envs (re-stored below)
+    const bool fast = full && *bad_word == 0;
+
+    // ---- observations of the moved state + reward terms (:99-100)
+    float4 *red = reinterpret_cast<float4 *>(lds + BP::RED);
+    float *obs_rows = lds + BP::OBS;
+    if (row_on) {
+        float rowv[D];
+        RowOut ro;
+        bool unused = true;
+        if (__builtin_expect(fast, 1))
+            ro = observe_row_own<A, O, !OBS_ONLY, true>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
+                                                        lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
+                                                        rowv, pr, unused);
+        else
+            ro = observe_row_own<A, O, !OBS_ONLY, false>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
+                                                         lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
+                                                         rowv, pr, unused);
+        lds_row_write<D>(obs_rows + r * D, rowv);
+        if (!OBS_ONLY) red[r] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
+    }
+    __syncthreads();
+    STAMP(3);
+    float *gobs = in_sgpr(b.obs + e0 * (A * D));
+    if (OBS_ONLY) block_store(gobs, obs_rows, nrow * D, tid, NT);
+    const bool norm = !OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM);
+    if (!OBS_ONLY) {
+        int *list = reinterpret_cast<int *>(lds + BP::LIST);
+        int *flg = reinterpret_cast<int *>(lds + BP::FLG);
+        const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
+        // native (non-noisy) re-init: waves 1..A-1 take the finished envs
+        // while wave 0 runs the per-env phase (below)
+        const bool overlap = !NOISY && !kargs_late()->a.b.fresh_states;
+        // ---- per-env reductions, terminal logic (wave 0, one lane per env)
+        if (w == 0) {
+            const bool env_on = l < ne;
+            bool fin = false, tr_l = false, co_l = false, ta_l = false;
+            if (env_on) {
+                const int64_t e = e0 + l;
+                float4 rr[A];
+#pragma unroll
+                for (int i = 0; i < A; ++i) rr[i] = red[A * l + i];
+                unsigned any_col = 0u, all_in = 1u;
+#pragma unroll
+                for (int i = 0; i < A; ++i) {
+                    const unsigned f = __float_as_uint(rr[i].z);
+                    any_col |= f & 1u;
+                    all_in &= (f >> 1) & 1u;
+                }
+                float rv[A];
+#pragma unroll
+                for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
+                const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
+                out_st(&b.reward[e], rsum / (float)A);                     // torch.mean (:233)
+
+                float step_num = lds[BP::SN + l] + 1.0f;           // :96
+                const bool truncated = step_num > pr.trunc_after;  // :97
+                const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
+                const bool terminated = any_col || term_old;       // :213-214
+                out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
+                out_st(&b.terminated[e], (uint8_t)terminated);
+                out_st(&b.truncated[e], (uint8_t)truncated);
+                fin = truncated || terminated;                     // :102-104
+                if (NOISY && fin) {  // noisy native re-init: serial per env
+                    KArgsK *kl = kargs_late();
+                    {
+                        MarlnavParams p;  // the fields the re-init reads
+                        p.obs_range_x = kl->p.obs_range_x;
+                        p.obs_mean_x = kl->p.obs_mean_x;
+                        p.obs_range_y = kl->p.obs_range_y;
+                        p.obs_mean_y = kl->p.obs_mean_y;
+                        p.ags_dist = kl->p.ags_dist;
+                        p.noise_std = kl->p.noise_std;
+                        p.angle_range = kl->p.angle_range;
+                        p.flags = kl->p.flags;
+                        p.seed = kl->p.seed;
+                        float *obl = lds + BP::OB + 2 * O * l;
+                        float *tgl = lds + BP::TG + 2 * l;
+                        native_fresh_env<NOISY>(A, O, p, lds + BP::FORM,
+                                                (uint64_t)(kl->a.env_offset + e), kl->a.step_idx,
+                                                st + 5 * A * l, obl, tgl);
+                        float *gob = kl->a.b.obstacles;
+                        for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
+                        kl->a.b.target[2 * e] = tgl[0];
+                        kl->a.b.target[2 * e + 1] = tgl[1];
+                    }
+                }
+                out_st(&b.step_num[e], fin ? blend_in(step_num, 0.0f) : step_num);
+                tr_l = truncated;
+                co_l = any_col;
+                ta_l = all_in;
+            }
+            const uint64_t finmask = __ballot(fin);
+            if (fin)
+                list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] = l;
+            const unsigned c_trunc = __popcll(__ballot(tr_l));
+            const unsigned c_col = __popcll(__ballot(co_l));
+            const unsigned c_tar = __popcll(__ballot(ta_l));
+            if (lane == 0) {
+                flg[0] = (int)__popcll(finmask);
+                if (c_trunc | c_col | c_tar) {
+                    KArgsK *kl = kargs_late();
+                    uint64_t *cnt = kl->a.b.counters;
+                    const int64_t slots = kl->a.waves;
+                    if (cnt) {
+                        const int64_t sl = blk % slots;
+                        if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
+                        if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + sl], (unsigned long long)c_col);
+                        if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
+                    }
+                }
+            }
+        } else if (overlap) {
+            // ---- waves 1..A-1, while wave 0 runs the per-env phase: the
+            // finished set from the inputs wave 0 uses (red flags, step_num,
+            // terminates), then the native re-init (:104) and re-observation
+            // (:105) of those envs. Disjoint LDS: wave 0 reads red/SN/TM; this
+            // writes the states, obstacles, target and rows of finished envs.
+            bool fin = false;
+            if (l < ne) {
+                unsigned any_col = 0u;
+#pragma unroll
+                for (int i = 0; i < A; ++i) any_col |= __float_as_uint(red[A * l + i].z) & 1u;
+                fin = lds[BP::SN + l] + 1.0f > pr.trunc_after || any_col != 0u ||
+                      reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
+            }
+            const uint64_t fm = __ballot(fin);
+            if (fm) {
+                int *wlist = reinterpret_cast<int *>(lds + BP::LIST2) + E * (w - 1);
+                if (fin)
+                    wlist[__builtin_amdgcn_mbcnt_hi(
+                        (unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] = l;
+                wave_sync();  // every lane of this wave sees its list
+                reinit_reobs_native<A, O>(kargs_late(), ev, lds + BP::FORM, wlist,
+                                          (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
+            }
+        }
+        __syncthreads();
+        STAMP(4);
+        const int nfin = flg[0];
+        if (nfin && !overlap) {
+            // ---- reference-RNG / noisy re-init (:104; noisy: done above by
+            // wave 0) and observations of the re-initialised envs (:105)
+            if (!NOISY) {
+                reinit_block<A, O>(kargs_late(), ev, lds + BP::FORM, list, nfin, tid, NT);
+                __syncthreads();
+            }
+            reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, NT);
+            __syncthreads();
+        }
+    }
+    STAMP(5);
+    if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
+        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
+                                               st, tid);  // (E = 64: whole 16-byte pieces)
+    } else if (!OBS_ONLY) {
+        block_store(gobs, obs_rows, nrow * D, tid, NT);
+        if (norm) {
+            KArgsK *kl = kargs_late();
+            const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
+            float *gn = kl->a.b.obs_norm + e0 * (A * D);
+            for (int i = tid; i < nrow * D; i += NT) {
+                const int kk = i % D;
+                gn[i] = (obs_rows[i] - mean[kk]) / scale[kk];
+            }
+        }
+        block_store(in_sgpr(b.states + e0 * (A * 5)), st, nrow * 5, tid, NT);
+    }
+    STAMP(6);
+#if MARLNAV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(7);
+    if (lane == 0) {
+        g_stamps[(size_t)gw * 24 + 16] = t_entry;
+        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 19] = OBS_ONLY ? 0u : (unsigned)reinterpret_cast<const int *>(lds + BP::FLG)[0];
+    }
+#endif
+    (void)gw;
+}

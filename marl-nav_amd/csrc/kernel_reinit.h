@@ -1,0 +1,306 @@
+// kernel_reinit.h - workgroup-spread re-initialisation and re-observation of finished envs (environment.py:76-90, 105), shared by the split and block kernels.
+// Part of libmarlnav.so: included once, by marlnav_step.hip (one translation
+// unit), inside its anonymous namespace.
+#pragma once
+
+// ------------------------------------- workgroup-spread re-init / re-observe
+// Where the block-spread re-init / re-observation below finds an env of the
+// workgroup: `c` is an env code from the finished-env list. BlockEnvs: the
+// env-block kernel's block-wide arrays (code = env within the block);
+// SplitEnvs: the pair-split kernel's wave-private tiles (code = wave * EPW +
+// env within the wave's tile, the tiles of a workgroup being consecutive).
+template <int A, int O, int RS>
+struct BlockEnvs {
+    float *st, *ob, *tg, *rows;
+    int64_t e0;
+    __device__ float *state(int c) const { return st + 5 * A * c; }
+    __device__ float *obst(int c) const { return ob + 2 * O * c; }
+    __device__ float *targ(int c) const { return tg + 2 * c; }
+    __device__ float *row(int c, int ag) const { return rows + (c * A + ag) * RS; }
+    __device__ int64_t env(int c) const { return e0 + c; }
+};
+
+template <int A, int O, int EPW, int FLOATS, int ST, int OB, int TG, int OBS, int RS>
+struct SplitEnvs {
+    float *lds;
+    int64_t e0;
+    __device__ float *wave(int c) const { return lds + (c / EPW) * FLOATS; }
+    __device__ float *state(int c) const { return wave(c) + ST + 5 * A * (c % EPW); }
+    __device__ float *obst(int c) const { return wave(c) + OB + 2 * O * (c % EPW); }
+    __device__ float *targ(int c) const { return wave(c) + TG + 2 * (c % EPW); }
+    __device__ float *row(int c, int ag) const { return wave(c) + OBS + ((c % EPW) * A + ag) * RS; }
+    __device__ int64_t env(int c) const { return e0 + c; }
+};
+
+// Re-observation of the finished envs (environment.py:105) spread over the
+// workgroup: one (row, pair) item per thread per pass, results written
+// straight into the packed rows. Per wave and pass, the short sqrt/division
+// sequences run when every coordinate of the pass passes coord_ok, IEEE
+// otherwise.
+template <int A, int O, class Envs, class List>
+__device__ __forceinline__ void reobs_block(const Envs &ev, const List &list, int nfin, float cap,
+                                            int tid, int nt)
+{
+    constexpr int NP = 1 + O + (A - 1);
+    const int nw = nfin * A * NP;
+    for (int base = 0; base < nw; base += nt) {
+        const int w = base + tid;
+        const bool on = w < nw;
+        const int wc = on ? w : 0;
+        const int fe = wc / (A * NP), rem = wc - fe * (A * NP);
+        const int ag = rem / NP, p = rem - ag * NP;
+        const int c = list[fe];
+        const float *s = ev.state(c) + 5 * ag;
+        const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
+        const float *pt;
+        int sa, sd;
+        if (p == 0) {            // target
+            pt = ev.targ(c);
+            sa = 0;
+            sd = 1;
+        } else if (p <= O) {     // obstacle p - 1
+            pt = ev.obst(c) + 2 * (p - 1);
+            sa = 1 + p;
+            sd = 1 + O + p;
+        } else {                 // other agent kx, skipping self
+            const int kx = p - O - 1;
+            pt = ev.state(c) + 5 * (kx + (kx >= ag ? 1 : 0));
+            sa = 2 + 2 * O + kx;
+            sd = 2 + 2 * O + (A - 1) + kx;
+        }
+        const float px = pt[0], py = pt[1];
+        const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+        bool unused = true;
+        float d, ang;
+        if (__ballot(on && !cok) == 0ull) {
+            d = pair_dist<true>(ox, oy, px, py, unused);
+            ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+        } else {
+            d = pair_dist<false>(ox, oy, px, py, unused);
+            ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+        }
+        if (on) {
+            float *o = ev.row(c, ag);
+            o[sa] = ang;
+            o[sd] = d;
+        }
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void lds_row_write(float *dst, const float *row)
+{
+    if constexpr (D % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 4)
+            *reinterpret_cast<float4 *>(dst + k) = make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]);
+    } else if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < D; k += 2)
+            *reinterpret_cast<float2 *>(dst + k) = make_float2(row[k], row[k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) dst[k] = row[k];
+    }
+}
+
+// Re-initialisation of the finished envs (environment.py:76-90, the sampler
+// call at :78) spread over the workgroup: one item per thread per pass - one
+// float of a fresh candidate (reference RNG) or of the formation template,
+// or one Philox block of two obstacles (native; the same draws as
+// native_fresh_env). Writes the LDS state and the global obstacles / target;
+// the agent rows go out with the final stores.
+template <int A, int O, class Envs, class List>
+__device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const float *form,
+                                             const List &list, int nfin, int tid, int nt)
+{
+    float *gob = kl->a.b.obstacles;
+    float *gtg = kl->a.b.target;
+    const float *fs = kl->a.b.fresh_states;
+    if (fs) {
+        const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
+        const bool keep = (kl->p.flags & MARLNAV_FRESH_STATES_FROM_MOVED) != 0;
+        constexpr int NI = 5 * A + 2 * O + 2;
+        for (int i = tid; i < nfin * NI; i += nt) {
+            const int fe = i / NI, kk = i - fe * NI;
+            const int c = list[fe];
+            const int64_t e = ev.env(c);
+            if (kk < 5 * A) {
+                float *d = ev.state(c) + kk;
+                *d = blend_in(*d, keep ? *d : fs[e * A * 5 + kk]);
+            } else if (kk < 5 * A + 2 * O) {
+                const int j = kk - 5 * A;
+                float *d = ev.obst(c) + j;
+                const float v = blend_in(*d, fo[e * O * 2 + j]);
+                *d = v;
+                gob[e * O * 2 + j] = v;
+            } else {
+                const int j = kk - 5 * A - 2 * O;
+                float *d = ev.targ(c) + j;
+                const float v = blend_in(*d, ft[2 * e + j]);
+                *d = v;
+                gtg[2 * e + j] = v;
+            }
+        }
+        return;
+    }
+    constexpr int NB = (O + 1) / 2, NI = 5 * A + 2 + NB;
+    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
+    const int64_t eoff = kl->a.env_offset;
+    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
+    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
+    for (int i = tid; i < nfin * NI; i += nt) {
+        const int fe = i / NI, kk = i - fe * NI;
+        const int c = list[fe];
+        const int64_t e = ev.env(c);
+        if (kk < 5 * A) {
+            float *d = ev.state(c) + kk;
+            *d = blend_in(*d, form[kk]);
+        } else if (kk < 5 * A + 2) {
+            const int j = kk - 5 * A;
+            float *d = ev.targ(c) + j;
+            const float v = blend_in(*d, form[kk]);
+            *d = v;
+            gtg[2 * e + j] = v;
+        } else {
+            const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
+            const uint64_t gid = (uint64_t)(eoff + e);
+            uint32_t cc[4] = {(uint32_t)jb, (uint32_t)sidx, (uint32_t)gid,
+                              (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
+            philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
+            const int j = 2 * jb;
+            float *o = ev.obst(c) + 2 * j;
+            float *g = gob + e * O * 2 + 2 * j;
+            o[0] = g[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+            o[1] = g[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
+            if (j + 1 < O) {
+                o[2] = g[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+                o[3] = g[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
+            }
+        }
+    }
+}
+
+// Native (non-noisy) re-init and re-observation of the finished envs in ONE
+// pass over the workgroup: a fresh env's agent rows and target are the
+// formation template and its obstacles are Philox draws (the same as
+// native_fresh_env), so each observation item computes its own inputs
+// instead of waiting for a re-init pass and a barrier. Items per finished
+// env: A*(1+O+A-1) pairs (written into the packed rows), 5A+2 template
+// floats and ceil(O/2) Philox blocks (written to the LDS state and the
+// global obstacles/target).
+template <int A, int O, class Envs, class List>
+__device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, const float *form,
+                                                    const List &list, int nfin, float cap, int tid,
+                                                    int nt)
+{
+    constexpr int NP = 1 + O + (A - 1), NB = (O + 1) / 2;
+    constexpr int NPAIR = A * NP, NI = NPAIR + 5 * A + 2 + NB;
+    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
+    const int64_t eoff = kl->a.env_offset;
+    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
+    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
+    float *gob = kl->a.b.obstacles;
+    float *gtg = kl->a.b.target;
+    const int n = nfin * NI;
+    for (int base = 0; base < n; base += nt) {
+        const int i = base + tid;
+        const bool on = i < n;
+        const int ic = on ? i : 0;
+        const int fe = ic / NI, kk = ic - fe * NI;
+        const int c = list[fe];
+        const int64_t e = ev.env(c);
+        const uint64_t gid = (uint64_t)(eoff + e);
+        const bool pair = kk < NPAIR;
+        // Philox block: obstacle pair items (the block of their obstacle) and
+        // obstacle store items
+        int jb = -1;
+        int ag = 0, p = 0;
+        if (pair) {
+            ag = kk / NP;
+            p = kk - ag * NP;
+            if (p >= 1 && p <= O) jb = (p - 1) >> 1;
+        } else if (kk >= NPAIR + 5 * A + 2) {
+            jb = kk - (NPAIR + 5 * A + 2);
+        }
+        uint32_t cc[4] = {0u, 0u, 0u, 0u};
+        if (jb >= 0) {
+            cc[0] = (uint32_t)jb;
+            cc[1] = (uint32_t)sidx;
+            cc[2] = (uint32_t)gid;
+            cc[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
+            philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
+        }
+        if (pair) {
+            // inputs: the blend of the env's current value (LDS; other items
+            // may be blending it in place meanwhile - blend_in is idempotent)
+            // with its fresh value (template or Philox draw)
+            const float *s = form + 5 * ag;
+            const float *so = ev.state(c) + 5 * ag;
+            const float ox = blend_in(so[0], s[0]), oy = blend_in(so[1], s[1]);
+            const float dx = blend_in(so[2], s[2]), dy = blend_in(so[3], s[3]);
+            float px, py;
+            int sa, sd;
+            if (p == 0) {            // target
+                px = blend_in(ev.targ(c)[0], form[5 * A]);
+                py = blend_in(ev.targ(c)[1], form[5 * A + 1]);
+                sa = 0;
+                sd = 1;
+            } else if (p <= O) {     // obstacle p - 1: components of its Philox block
+                const bool hi = ((p - 1) & 1) != 0;
+                const uint32_t ux = hi ? cc[2] : cc[0], uy = hi ? cc[3] : cc[1];
+                const float *oo = ev.obst(c) + 2 * (p - 1);
+                px = blend_in(oo[0], rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx);
+                py = blend_in(oo[1], ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my);
+                sa = 1 + p;
+                sd = 1 + O + p;
+            } else {                 // other agent kx, skipping self
+                const int kx = p - O - 1;
+                const int m = kx + (kx >= ag ? 1 : 0);
+                const float *q = form + 5 * m;
+                const float *qo = ev.state(c) + 5 * m;
+                px = blend_in(qo[0], q[0]);
+                py = blend_in(qo[1], q[1]);
+                sa = 2 + 2 * O + kx;
+                sd = 2 + 2 * O + (A - 1) + kx;
+            }
+            const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+            bool unused = true;
+            float d, ang;
+            if (__ballot(on && !cok) == 0ull) {
+                d = pair_dist<true>(ox, oy, px, py, unused);
+                ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+            } else {
+                d = pair_dist<false>(ox, oy, px, py, unused);
+                ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+            }
+            if (on) {
+                float *o = ev.row(c, ag);
+                o[sa] = ang;
+                o[sd] = d;
+            }
+        } else if (on) {
+            const int k2 = kk - NPAIR;
+            if (k2 < 5 * A) {
+                float *d = ev.state(c) + k2;
+                *d = blend_in(*d, form[k2]);
+            } else if (k2 < 5 * A + 2) {
+                const int j = k2 - 5 * A;
+                float *d = ev.targ(c) + j;
+                const float v = blend_in(*d, form[k2]);
+                *d = v;
+                gtg[2 * e + j] = v;
+            } else {
+                const int j = 2 * jb;
+                float *o = ev.obst(c) + 2 * j;
+                float *g = gob + e * O * 2 + 2 * j;
+                o[0] = g[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+                o[1] = g[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
+                if (j + 1 < O) {
+                    o[2] = g[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+                    o[3] = g[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
+                }
+            }
+        }
+    }
+}

@@ -1,0 +1,632 @@
+// kernel_split.h - pair-split kernel (LPR lanes per agent row: A16/O32, small A3 grids).
+// Part of libmarlnav.so: included once, by marlnav_step.hip (one translation
+// unit), inside its anonymous namespace.
+#pragma once
+
+// ------------------------------------------------------ pair-split kernel
+// For shapes whose rows carry many pairs (A16/O32: 48 per row) or grids too
+// small to fill the chip with one lane per row: LPR lanes share each agent
+// row. Lane q of a row evaluates the target pair (kept by q == 0), obstacles
+// q, q+LPR, ... and other agents q, q+LPR, ...; the packed observation rows
+// are assembled in LDS and streamed out with vector stores; per-row flags
+// and counts are OR/sum-reduced across the LPR lanes with DPP / swizzles;
+// the row's bond terms (environment.py:264-269) are evaluated by the lanes
+// that own the distances and summed by the row leader in torch's order.
+// LDS row stride of the split kernel's packed observation rows: D padded
+// (keeping 16-byte row alignment when D % 4 == 0) so that the LPR lanes of
+// each of the 32/LPR rows in a ds_write_b32 lane group hit distinct banks
+// ((a/4) mod 32, MI355X_MICROARCH.md §LDS). At A16/O32 (D = 96) unpadded rows
+// are 8-way conflicted: every row starts on bank 0.
+__host__ __device__ constexpr int split_conflicts(int s, int LPR, int rows)
+{
+    int worst = 0;
+    for (int b = 0; b < 32; ++b) {
+        int n = 0;
+        for (int l = 0; l < 32; ++l) {
+            const int r = l / LPR, q = l % LPR;
+            if (r < rows && (r * s + q) % 32 == b) ++n;
+        }
+        worst = n > worst ? n : worst;
+    }
+    return worst;
+}
+
+__host__ __device__ constexpr int split_row_stride(int D, int LPR, int rows)
+{
+    if (D % 4 != 0) return D;  // rows stored with 4/8-byte pieces: keep them dense
+    int best = D, bc = split_conflicts(D, LPR, rows);
+    for (int s = D + 4; s <= D + 32; s += 4) {
+        const int c = split_conflicts(s, LPR, rows);
+        if (c < bc) {
+            best = s;
+            bc = c;
+        }
+    }
+    return best;
+}
+
+
+// Finished envs of a split-kernel workgroup: wave w listed cnt[w] env codes
+// (w * EPW + env) in slot[w * EPW ...]; entry fe of the concatenation.
+template <int EPW>
+struct SplitFinList {
+    int off1, off2, off3, n;  // prefix sums over the (up to 4) live waves
+    const int *slot;
+    __device__ static SplitFinList make(const int *cnt, const int *slot, int live)
+    {
+        static_assert(kWavesPerBlock == 4, "four waves per workgroup");
+        const int c0 = cnt[0];
+        const int c1 = live > 1 ? cnt[1] : 0;
+        const int c2 = live > 2 ? cnt[2] : 0;
+        const int c3 = live > 3 ? cnt[3] : 0;
+        return SplitFinList{c0, c0 + c1, c0 + c1 + c2, c0 + c1 + c2 + c3, slot};
+    }
+    __device__ int total() const { return n; }
+    __device__ int operator[](int fe) const
+    {
+        const int w = (fe >= off1) + (fe >= off2) + (fe >= off3);
+        const int base = w == 0 ? 0 : (w == 1 ? off1 : (w == 2 ? off2 : off3));
+        return slot[w * EPW + fe - base];
+    }
+};
+
+// Finished envs re-initialised and re-observed by the whole workgroup
+// (after one block barrier) instead of by their own wave: pays where an
+// env's re-observation is long (measured: A3/O8 and A16/O32 faster, A3/O3
+// slower). MARLNAV_SPLIT_SPREAD=0 turns it off (A/B builds).
+template <int A, int O>
+constexpr bool kSplitSpread = A * (1 + O + (A - 1)) >= 32;
+
+template <int A, int O, int LPR>
+struct SplitPlan {
+    static constexpr int EPW = 64 / LPR / A;  // envs per wave
+    static constexpr int R = EPW * A;         // rows per wave
+    static constexpr int D = 2 + 2 * O + 2 * (A - 1);
+    static constexpr int NOB = (O + LPR - 1) / LPR;        // obstacle pairs per lane
+    static constexpr int NAG = (A - 1 + LPR - 1) / LPR;    // other-agent pairs per lane
+    static constexpr int ST = 0;                           // (R, 5)
+    static constexpr int ACT = (ST + R * 5 + 3) & ~3;      // (R, 2)
+    static constexpr int OB = (ACT + R * 2 + 3) & ~3;      // (EPW, O, 2)
+    static constexpr int TG = (OB + EPW * O * 2 + 3) & ~3; // (EPW, 2)
+    static constexpr int SN = (TG + EPW * 2 + 3) & ~3;     // (EPW,)
+    static constexpr int DP = split_row_stride(D, LPR, R < 32 / LPR ? R : 32 / LPR);
+    static constexpr int OBS = (SN + EPW + 3) & ~3;        // (R, DP)
+    static constexpr int BOND = (OBS + R * DP + 3) & ~3;   // (R, A-1)
+    static constexpr int RED = (BOND + R * (A - 1) + 3) & ~3;  // (R, 4)
+    static constexpr int FLOATS = RED + 4 * R;
+    // after the waves' regions: finished-env counts and slots of the workgroup
+    static constexpr int BLK = (kWavesPerBlock * (1 + EPW) + 3) & ~3;
+    static_assert(EPW >= 1, "an env's rows must fit one wave");
+};
+
+__host__ __device__ constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
+
+// the fast pair math pays for its per-wave coordinate check only with many
+// pairs per lane (measured: A16/O32 yes, A3/O3 and A3/O8 at LPR 4 no)
+template <int A, int O, int LPR>
+constexpr bool kSplitFastMath = SplitPlan<A, O, LPR>::NOB + SplitPlan<A, O, LPR>::NAG >= 6;
+
+// global -> LDS copy of NB bytes whose source is ALIGN-byte aligned: 16-byte
+// LDS-DMA when possible, else dword LDS-DMA (NB % 4 == 0, ALIGN % 4 == 0).
+template <int NB, int ALIGN>
+__device__ __forceinline__ void glds_span_aligned(const void *src, float *dst, unsigned lane)
+{
+    if constexpr (ALIGN % 16 == 0) {
+        glds_span<NB>(src, dst, lane);
+    } else {
+        static_assert(NB % 4 == 0 && ALIGN % 4 == 0, "dword-aligned span");
+        constexpr int N4 = NB / 4;
+#pragma unroll
+        for (int kk = 0; kk * 64 < N4; ++kk) {
+            const char *s = in_sgpr(reinterpret_cast<const char *>(src) + kk * 256);
+            if ((kk + 1) * 64 <= N4 || (int)lane < N4 - kk * 64)
+                __builtin_amdgcn_global_load_lds(s + lane * 4u, (LdsVoid *)(dst + kk * 64), 4, 0, 0);
+        }
+    }
+}
+
+// OR / sum over the LPR consecutive lanes of a row (LPR a power of two)
+template <int LPR>
+__device__ __forceinline__ unsigned lpr_or(unsigned v)
+{
+    if constexpr (LPR >= 2) v |= (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    if constexpr (LPR >= 4) v |= (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    if constexpr (LPR >= 8) v |= (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);
+    if constexpr (LPR >= 16) v |= (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x201F);
+    return v;
+}
+
+template <int LPR>
+__device__ __forceinline__ int lpr_sum(int v)
+{
+    if constexpr (LPR >= 2) v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+    if constexpr (LPR >= 4) v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+    if constexpr (LPR >= 8) v += __builtin_amdgcn_ds_swizzle(v, 0x101F);
+    if constexpr (LPR >= 16) v += __builtin_amdgcn_ds_swizzle(v, 0x201F);
+    return v;
+}
+
+// This lane's pairs of its row: distances and bearings into the LDS row
+// `orow`; with TERMS also the per-lane reward flags and bond terms.
+struct SplitTerms {
+    unsigned fl;  // 1 ob_risk, 2 ob_col, 4 ag_risk, 8 ag_col
+    int band;
+    float ta, td;
+};
+
+// Occupancy the register allocator may assume (waves per SIMD): the grids
+// below run at most 3-4 waves per SIMD, so the default target of 8 only
+// costs instruction-level parallelism (timing builds set these).
+
+// The target pair takes a spare slot of lane LPR-1 when the other agents (or
+// else the obstacles) do not divide over the LPR lanes: one pair body fewer per
+// wave (A16/O32: 13 -> 12, A3/O8: 4 -> 3); the row leader reads the target
+// angle/distance back from the LDS row.
+template <int A, int O, int LPR>
+constexpr bool kSplitTgtInAg = (A - 1) % LPR != 0;
+template <int A, int O, int LPR>
+constexpr bool kSplitTgtInOb = !kSplitTgtInAg<A, O, LPR> && O % LPR != 0;
+
+// unroll factor of split_pairs' obstacle / other-agent loops (timing builds)
+
+template <int A, int O, int LPR, bool TERMS, bool FAST>
+__device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
+                                                  const float *__restrict__ obe,
+                                                  const float *__restrict__ tge, int a, int q,
+                                                  float ox, float oy, float dx, float dy,
+                                                  float *__restrict__ orow,
+                                                  float *__restrict__ bond_row,
+                                                  const MarlnavParams &pr, bool &ok)
+{
+    using SP = SplitPlan<A, O, LPR>;
+    constexpr int TQ = LPR - 1;  // the lane whose last other-agent / obstacle slot is spare
+    const float cap = pr.cap_distance;
+    SplitTerms t{0u, 0, 0.0f, 0.0f};
+    if constexpr (!kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>) {
+        const float d = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
+        const float ang = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, d, cap, ok);
+        t.ta = ang;
+        t.td = d;
+        if (q == 0) {
+            orow[0] = ang;
+            orow[1] = d;
+        }
+    }
+#pragma unroll 64
+    for (int i = 0; i < SP::NOB; ++i) {
+        const int j = q + LPR * i;
+        constexpr bool spare = kSplitTgtInOb<A, O, LPR>;
+        const bool last = i == SP::NOB - 1;
+        const bool valid = O % LPR == 0 || j < O;
+        const bool tgt = spare && last && q == TQ;  // j >= O there: the target pair
+        if (valid || tgt) {
+            const float *pt = tgt ? tge : obe + 2 * (valid ? j : 0);
+            const float px = pt[0], py = pt[1];
+            const float d = pair_dist<FAST>(ox, oy, px, py, ok);
+            const float ang = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
+            if (valid) {
+                orow[2 + j] = ang;
+                orow[2 + O + j] = d;
+                if (TERMS)
+                    t.fl |= (d < pr.ob_risk_dist ? 1u : 0u) | (d < pr.ob_coll_dist ? 2u : 0u);
+            } else {
+                orow[0] = ang;
+                orow[1] = d;
+            }
+        }
+    }
+#pragma unroll 64
+    for (int i = 0; i < SP::NAG; ++i) {
+        const int kx = q + LPR * i;  // index among the others
+        constexpr bool spare = kSplitTgtInAg<A, O, LPR>;
+        const bool last = i == SP::NAG - 1;
+        const bool valid = (A - 1) % LPR == 0 || kx < A - 1;
+        const bool tgt = spare && last && q == TQ;  // kx >= A - 1 there: the target pair
+        if (valid || tgt) {
+            const int m = valid ? kx + (kx >= a ? 1 : 0) : 0;
+            const float *pt = tgt ? tge : sts + 5 * m;
+            const float px = pt[0], py = pt[1];
+            const float d = pair_dist<FAST>(ox, oy, px, py, ok);
+            const float ang = pair_angle<FAST>(ox, oy, px, py, dx, dy, d, cap, ok);
+            if (!valid) {
+                orow[0] = ang;
+                orow[1] = d;
+            } else {
+                orow[2 + 2 * O + kx] = ang;
+                orow[2 + 2 * O + (A - 1) + kx] = d;
+                if (TERMS) {
+                    t.fl |= (d < pr.ag_risk_dist ? 4u : 0u) | (d < pr.ag_coll_dist ? 8u : 0u);
+                    t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
+                    const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
+                    bond_row[kx] = 1.0f / (1.0f + sd * sd);
+                }
+            }
+        }
+    }
+    return t;
+}
+
+template <int A, int O, int LPR, bool OBS_ONLY, bool NOISY>
+__global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
+{
+    using SP = SplitPlan<A, O, LPR>;
+    constexpr int EPW = SP::EPW, R = SP::R, D = SP::D;
+    (void)k;  // read through kargs_late()
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+#if MARLNAV_STAMPS
+    int stamp_nfin = 0;
+#endif
+#if MARLNAV_STAMPS
+    unsigned long long t_entry;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
+#endif
+    const unsigned lane = threadIdx.x & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wib;
+    const int64_t tile = gw;
+    KArgsK *K = kargs_late();
+    const int64_t P = K->a.P;
+    // pointers first, pinned in SGPRs before the exit test: one round of
+    // kernarg loads ahead of the first wait (the compiler would otherwise
+    // sink them below the branch, a second serial round)
+    const StepPtrs b = load_ptrs(K);
+    const int64_t ntiles = K->a.ntiles;
+    asm volatile("" ::"s"(b.states), "s"(b.obstacles), "s"(b.target), "s"(b.actions),
+                 "s"(b.obs), "s"(ntiles), "s"(P));
+    if (tile >= ntiles) return;
+    STAMP(0);
+    float *wl = lds + wib * SP::FLOATS;
+    float *st = wl + SP::ST;
+    const int64_t e0 = tile * EPW;
+    const int ne = (int)((P - e0) < EPW ? (P - e0) : EPW);
+    const int nr = ne * A;
+
+    // ---- stage the tile (the per-env scalars go straight to the env lanes)
+    if (ne == EPW) {
+        glds_span_aligned<R * 20, gcd_c(R * 20, 16)>(b.states + e0 * (A * 5), st, lane);
+        if (!OBS_ONLY)
+            glds_span_aligned<R * 8, gcd_c(R * 8, 16)>(b.actions + e0 * (A * 2), wl + SP::ACT, lane);
+        glds_span_aligned<EPW * O * 8, gcd_c(EPW * O * 8, 16)>(b.obstacles + e0 * (O * 2),
+                                                              wl + SP::OB, lane);
+        glds_span_aligned<EPW * 8, gcd_c(EPW * 8, 16)>(b.target + e0 * 2, wl + SP::TG, lane);
+    } else {
+        copy_span(b.states + e0 * (A * 5), st, nr * 5, (int)lane);
+        if (!OBS_ONLY) copy_span(b.actions + e0 * (A * 2), wl + SP::ACT, nr * 2, (int)lane);
+        copy_span(b.obstacles + e0 * (O * 2), wl + SP::OB, ne * O * 2, (int)lane);
+        copy_span(b.target + e0 * 2, wl + SP::TG, ne * 2, (int)lane);
+    }
+    const bool env_on = (int)lane < ne;
+    float sn_in = 0.0f;
+    unsigned term_in = 0u;
+    if (!OBS_ONLY && env_on) {
+        sn_in = b.step_num[e0 + lane];
+        term_in = b.terminates[e0 + lane];
+    }
+    const MarlnavParams pr = load_params(K);
+    const int row = (int)lane / LPR, q = (int)lane - row * LPR;
+    const int rowc = row < R ? row : 0;  // idle lanes shadow row 0 (results unused)
+    const int el = rowc / A, a = rowc - el * A;
+    const bool row_on = row < nr;
+    unsigned c_trunc = 0, c_col = 0, c_tar = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
+    wave_sync();
+    STAMP(1);
+
+    // ---- _move_agents (environment.py:113-123): every lane of a row moves
+    // it (same instructions either way), the row leader stores it
+    float ox = st[5 * rowc], oy = st[5 * rowc + 1];
+    float dx = st[5 * rowc + 2], dy = st[5 * rowc + 3];
+    if (!OBS_ONLY) {
+        const float2 act = reinterpret_cast<const float2 *>(wl + SP::ACT)[rowc];
+        float a0 = act.x, a1 = act.y;
+        if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
+            KArgsK *kl = kargs_late();
+            a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
+            a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
+        }
+        float sn, c;
+        sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+        const float ndx = c * dx + (-sn) * dy;
+        const float ndy = sn * dx + c * dy;
+        const float v = clamp_t(st[5 * rowc + 4] + clamp_t(a1, pr.min_accel, pr.max_accel),
+                                pr.min_speed, pr.max_speed);
+        ox = ox + ndx * v;
+        oy = oy + ndy * v;
+        dx = ndx;
+        dy = ndy;
+        wave_sync();  // every lane has read the pre-move rows
+        if (row_on && q == 0) {
+            float *s = st + 5 * row;
+            s[0] = ox;
+            s[1] = oy;
+            s[2] = dx;
+            s[3] = dy;
+            s[4] = v;
+        }
+        wave_sync();
+    }
+    STAMP(2);
+
+    // ---- observations + per-lane reward terms (:99-100)
+    const float *sts = st + 5 * A * el;
+    const float *obe = wl + SP::OB + 2 * O * el;
+    const float *tge = wl + SP::TG + 2 * el;
+    float *orow = wl + SP::OBS + rowc * SP::DP;
+    float *brow = wl + SP::BOND + rowc * (A - 1);
+    {
+        // wave-uniform choice of the pair math (coord_ok);
+        // worth its check only when each lane evaluates many pairs
+        bool fast = false;
+        if constexpr (kSplitFastMath<A, O, LPR>) {
+            const bool cok = (!row_on || (coord_ok(ox) && coord_ok(oy))) &&
+                             tile_coords_ok<EPW * O * 2, EPW * 2>(wl + SP::OB, wl + SP::TG, lane);
+            fast = ne == EPW && __ballot(!cok) == 0ull;
+        }
+        bool unused = true;
+        SplitTerms t;
+        if (__builtin_expect(fast, 1))
+            t = split_pairs<A, O, LPR, !OBS_ONLY, true>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
+                                                       brow, pr, unused);
+        else
+            t = split_pairs<A, O, LPR, !OBS_ONLY, false>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
+                                                        brow, pr, unused);
+        if (!OBS_ONLY) {
+            const unsigned fl = lpr_or<LPR>(t.fl);
+            const int band = lpr_sum<LPR>(t.band);
+            wave_sync();  // bond terms of the row are in LDS
+            if (row_on && q == 0) {
+                if constexpr (kSplitTgtInAg<A, O, LPR> || kSplitTgtInOb<A, O, LPR>) {
+                    t.ta = orow[0];  // computed by lane LPR-1 (wave_sync above)
+                    t.td = orow[1];
+                }
+                const float head = fabsf(t.ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+                const float bandf = (float)band;
+                const float bandc = bandf < pr.max_at_prop_d ? bandf : pr.max_at_prop_d;
+                float bv[A - 1];
+#pragma unroll
+                for (int i = 0; i < A - 1; ++i) bv[i] = brow[i];
+                const float bond = torch_row_sum_r<A - 1>(bv, [](float x) { return x; });
+                const float dsc = bandc / pr.max_at_prop_d;
+                const float soft = -1.0f * (t.td / pr.init_dist);
+                const float bondm = bond / (float)(A - 1);
+                const float risk = (fl & 5u) ? 1.0f : 0.0f;
+                float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
+                float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
+                rm = rm + pr.distance_factor * dsc;
+                rh = rh + pr.distance_factor * dsc;
+                rm = rm + pr.soft_factor * soft;
+                rh = rh + pr.soft_factor * soft;
+                rm = rm + pr.bond_factor * bondm;
+                rh = rh + pr.bond_factor * bondm;
+                rm = rm - pr.risk_factor * risk;
+                rh = rh - pr.risk_factor * risk;
+                const unsigned flags = ((fl & 10u) ? 1u : 0u) | ((t.td < pr.target_radius) ? 2u : 0u);
+                reinterpret_cast<float4 *>(wl + SP::RED)[row] =
+                    make_float4(rm, rh, __uint_as_float(flags), 0.0f);
+            }
+        }
+    }
+    STAMP(3);
+
+    if (!OBS_ONLY) {
+        wave_sync();
+        // ---- per-env reductions, terminal logic, masked re-init
+        bool fin = false, tr_l = false, co_l = false, ta_l = false;
+        if (env_on) {
+            const int64_t e = e0 + lane;
+            const float4 *red = reinterpret_cast<const float4 *>(wl + SP::RED) + A * lane;
+            unsigned any_col = 0u, all_in = 1u;
+            float rm[A], rh[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i) {
+                const float4 r = red[i];
+                const unsigned f = __float_as_uint(r.z);
+                any_col |= f & 1u;
+                all_in &= (f >> 1) & 1u;
+                rm[i] = r.x;
+                rh[i] = r.y;
+            }
+            float rv[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
+            const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
+            out_st(&b.reward[e], rsum / (float)A);             // torch.mean (:233)
+            float step_num = sn_in + 1.0f;                     // :96
+            const bool truncated = step_num > pr.trunc_after;  // :97
+            const bool term_old = term_in != 0u;
+            const bool terminated = any_col || term_old;       // :213-214
+            out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
+            out_st(&b.terminated[e], (uint8_t)terminated);
+            out_st(&b.truncated[e], (uint8_t)truncated);
+            fin = truncated || terminated;                     // :102-104
+            if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
+                KArgsK *kl = kargs_late();
+                MarlnavParams p;  // the fields the re-init reads
+                p.obs_range_x = kl->p.obs_range_x;
+                p.obs_mean_x = kl->p.obs_mean_x;
+                p.obs_range_y = kl->p.obs_range_y;
+                p.obs_mean_y = kl->p.obs_mean_y;
+                p.ags_dist = kl->p.ags_dist;
+                p.noise_std = kl->p.noise_std;
+                p.angle_range = kl->p.angle_range;
+                p.flags = kl->p.flags;
+                p.seed = kl->p.seed;
+                float *s5 = st + 5 * A * lane;
+                float *obl = wl + SP::OB + 2 * O * lane;
+                float *tgl = wl + SP::TG + 2 * lane;
+                const float *fs = kl->a.b.fresh_states;
+                float *gob = kl->a.b.obstacles;
+                float *gtg = kl->a.b.target;
+                if (!NOISY && fs) {
+                    const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
+                    const bool moved = (p.flags & MARLNAV_FRESH_STATES_FROM_MOVED) != 0;
+                    for (int i = 0; i < 5 * A; ++i)
+                        s5[i] = blend_in(s5[i], moved ? s5[i] : fs[e * A * 5 + i]);
+                    for (int i = 0; i < 2 * O; ++i) obl[i] = blend_in(obl[i], fo[e * O * 2 + i]);
+                    tgl[0] = blend_in(tgl[0], ft[2 * e]);
+                    tgl[1] = blend_in(tgl[1], ft[2 * e + 1]);
+                } else {
+                    native_fresh_env<NOISY>(A, O, p, kl->a.b.formation,
+                                            (uint64_t)(kl->a.env_offset + e), kl->a.step_idx, s5,
+                                            obl, tgl);
+                }
+                for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
+                gtg[2 * e] = tgl[0];
+                gtg[2 * e + 1] = tgl[1];
+            }
+            if (fin) step_num = blend_in(step_num, 0.0f);
+            out_st(&b.step_num[e], step_num);
+            tr_l = truncated;
+            co_l = any_col;
+            ta_l = all_in;
+        }
+        const uint64_t finmask = __ballot(fin);
+        c_trunc = __popcll(__ballot(tr_l));
+        c_col = __popcll(__ballot(co_l));
+        c_tar = __popcll(__ballot(ta_l));
+        STAMP(4);
+
+        if constexpr (kSplitSpread<A, O>) {
+            // ---- the workgroup's finished envs, re-initialised (:104) and
+            // re-observed (:105) by all its threads: a finished env costs its
+            // wave ~1/4 of a full observation pass instead of a second pass
+            // on its own lanes (the straggler that set the kernel's end)
+            int *bcnt = reinterpret_cast<int *>(lds + kWavesPerBlock * SP::FLOATS);
+            int *bslot = bcnt + kWavesPerBlock;
+            if (fin)
+                bslot[wib * EPW + (int)__builtin_amdgcn_mbcnt_hi(
+                                      (unsigned)(finmask >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] =
+                    wib * EPW + (int)lane;
+            if (lane == 0) bcnt[wib] = (int)__popcll(finmask);
+            __syncthreads();
+            const int64_t blk0 = (int64_t)blockIdx.x * kWavesPerBlock;
+            const int live = (int)(K->a.ntiles - blk0 < kWavesPerBlock ? K->a.ntiles - blk0
+                                                                      : kWavesPerBlock);
+            const SplitFinList<EPW> list = SplitFinList<EPW>::make(bcnt, bslot, live);
+#if MARLNAV_STAMPS
+            stamp_nfin = list.total();
+#endif
+            if (const int nfin = list.total()) {
+                KArgsK *kl = kargs_late();
+                const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
+                    lds, blk0 * EPW};
+                // waves past the last tile have exited: items go to the live ones
+                const int tid = (int)threadIdx.x, nt = 64 * live;
+                // fused native re-init + re-observation recomputes a Philox
+                // block per obstacle pair: only for few obstacles
+                if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
+                    reinit_reobs_native<A, O>(kl, ev, kl->a.b.formation, list, nfin,
+                                              pr.cap_distance, tid, nt);
+                } else {
+                    if (!NOISY) {
+                        reinit_block<A, O>(kl, ev, kl->a.b.formation, list, nfin, tid, nt);
+                        __syncthreads();
+                    }
+                    reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
+                }
+                __syncthreads();
+            }
+        } else if (finmask) {
+            // ---- observations of re-initialised envs (:105), on the wave
+            wave_sync();
+            const bool redo = row_on && ((finmask >> el) & 1u);
+            const float *s = st + 5 * rowc;
+            const float rx = s[0], ry = s[1], rdx = s[2], rdy = s[3];
+            bool fast2 = false;
+            if constexpr (kSplitFastMath<A, O, LPR>) {
+                const bool cok2 = (!redo || (coord_ok(rx) && coord_ok(ry))) &&
+                                  tile_coords_ok<EPW * O * 2, EPW * 2>(wl + SP::OB, wl + SP::TG, lane);
+                fast2 = ne == EPW && __ballot(!cok2) == 0ull;
+            }
+            bool unused = true;
+            if (redo) {
+                if (fast2)
+                    split_pairs<A, O, LPR, false, true>(sts, obe, tge, a, q, rx, ry, rdx, rdy,
+                                                       orow, brow, pr, unused);
+                else
+                    split_pairs<A, O, LPR, false, false>(sts, obe, tge, a, q, rx, ry, rdx, rdy,
+                                                        orow, brow, pr, unused);
+            }
+        }
+    }
+    STAMP(5);
+
+    // ---- stream the tile out (obs rows and states from LDS)
+    wave_sync();
+    {
+        const float *src = wl + SP::OBS;
+        float *gobs = in_sgpr(b.obs + e0 * (A * D));
+        const int n = nr * D;
+        constexpr int VAL = gcd_c(R * D * 4, 16);  // tile base alignment in bytes
+        float *gnorm = nullptr;
+        const float *mean = nullptr, *scale = nullptr;
+        if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
+            KArgsK *kl = kargs_late();
+            gnorm = kl->a.b.obs_norm + e0 * (A * D);
+            mean = kl->a.b.norm_mean;
+            scale = kl->a.b.norm_scale;
+        }
+        if constexpr (SP::DP != D) {  // padded rows (D % 4 == 0): 16-byte pieces
+            static_assert(D % 4 == 0 && SP::DP % 4 == 0, "padded rows keep 16-byte alignment");
+            constexpr int D4 = D / 4;
+            if (VAL % 16 == 0) {
+                for (int i = (int)lane; i < n / 4; i += 64) {
+                    const int rr = i / D4, c4 = i - rr * D4;
+                    out_st4<kNtRows>(gobs + 4 * i, *reinterpret_cast<const float4 *>(src + rr * SP::DP + 4 * c4));
+                }
+            } else {
+                for (int i = (int)lane; i < n; i += 64) {
+                    const int rr = i / D;
+                    out_st<kNtRows>(gobs + i, src[rr * SP::DP + (i - rr * D)]);
+                }
+            }
+        } else if (VAL % 16 == 0 && ne == EPW) {
+            for (int i = (int)lane; i < n / 4; i += 64)
+                out_st4<kNtRows>(gobs + 4 * i, reinterpret_cast<const float4 *>(src)[i]);
+        } else if (VAL % 8 == 0 && n % 2 == 0) {
+            for (int i = (int)lane; i < n / 2; i += 64)
+                out_st2<kNtRows>(gobs + 2 * i, reinterpret_cast<const float2 *>(src)[i]);
+        } else {
+            for (int i = (int)lane; i < n; i += 64) out_st<kNtRows>(gobs + i, src[i]);
+        }
+        if (gnorm)
+            for (int i = (int)lane; i < n; i += 64) {
+                const int rr = i / D, kk = i - rr * D;
+                gnorm[i] = (src[rr * SP::DP + kk] - mean[kk]) / scale[kk];
+            }
+    }
+    if (!OBS_ONLY) {
+        float *gst = in_sgpr(b.states + e0 * (A * 5));
+        const int n = nr * 5;
+        constexpr int SAL = gcd_c(R * 20, 16);
+        if (SAL % 16 == 0 && ne == EPW) {
+            for (int i = (int)lane; i < n / 4; i += 64)
+                out_st4<kNtRows>(gst + 4 * i, reinterpret_cast<const float4 *>(st)[i]);
+        } else {
+            for (int i = (int)lane; i < n; i += 64) out_st<kNtRows>(gst + i, st[i]);
+        }
+    }
+    STAMP(6);
+    if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
+        KArgsK *kl = kargs_late();
+        uint64_t *cnt = kl->a.b.counters;
+        const int64_t slots = kl->a.waves;
+        if (cnt) {
+            const int64_t sl = gw % slots;  // slots may be fewer than this grid's waves
+            if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
+            if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + sl], (unsigned long long)c_col);
+            if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
+        }
+    }
+#if MARLNAV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(7);
+    if (lane == 0) {
+        g_stamps[(size_t)gw * 24 + 16] = t_entry;
+        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+        g_stamps[(size_t)gw * 24 + 19] = (unsigned)stamp_nfin;
+    }
+#endif
+}

@@ -1,0 +1,26 @@
+// marlnav_debug.h - diagnostic stamps build (MARLNAV_STAMPS=1, scripts/kstamps.py); compiles to nothing otherwise.
+// Part of libmarlnav.so: included once, by marlnav_step.hip (one translation
+// unit), inside its anonymous namespace.
+#pragma once
+
+// Diagnostic build (MARLNAV_STAMPS=1, scripts/kstamps.py): lane 0 of every
+// wave records s_memrealtime / s_memtime at each phase boundary into a
+// buffer registered with marlnav_debug_stamps().
+#ifndef MARLNAV_STAMPS
+#define MARLNAV_STAMPS 0
+#endif
+#if MARLNAV_STAMPS
+__device__ unsigned long long *g_stamps;
+#define STAMP(k)                                                                   \
+    do {                                                                           \
+        if (lane == 0) {                                                           \
+            unsigned long long *sp_ = g_stamps + (size_t)gw * 24;                  \
+            sp_[2 * (k)] = wall_clock64();                                         \
+            sp_[2 * (k) + 1] = clock64();                                          \
+        }                                                                          \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
