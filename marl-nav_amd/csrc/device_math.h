@@ -250,35 +250,32 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
     return dist < cap ? 0.0f : ang;
 }
 
-// sin/cos of an angle already clamped to [-pi, pi], evaluated in double and
-// rounded once: Cody-Waite reduction by pi/2 (two-part constant, |k| <= 2)
-// and the fdlibm __kernel_sin/__kernel_cos minimax polynomials on
-// [-pi/4, pi/4]. Identical expression tree in oracle/marlnav_oracle.c.
+// sin/cos of an angle already clamped to [-pi, pi] in fp32 (<= 1 ulp, like
+// torch's SLEEF sin/cos on the reference's CPU path): three-part Cody-Waite
+// reduction by pi/2 (|k| <= 2, every product exact), the Cephes single-
+// precision minimax polynomials on [-pi/4, pi/4] (cosine with the 1 - z/2
+// rounding error carried), quadrant by comparisons (NaN -> quadrant 0, so
+// NaN propagates). The identical operation sequence is oracle_sincos in
+// oracle/marlnav_oracle.c (both built without FMA contraction), so kernel
+// and oracle agree bit for bit.
 __device__ __forceinline__ void sincos_k(float th, float *s_out, float *c_out)
 {
-    const double x = (double)th;
-    const double k = __builtin_rint(x * 6.36619772367581382433e-01);
-    double r = __builtin_fma(-k, 1.57079632679489655800e+00, x);
-    r = __builtin_fma(-k, 6.12323399573676603587e-17, r);
-    r = k == 0.0 ? x : r;  // keeps the sign of -0
-    const double z = r * r;
-    double ps = __builtin_fma(1.58969099521155010221e-10, z, -2.50507602534068634195e-08);
-    ps = __builtin_fma(ps, z, 2.75573137070700676789e-06);
-    ps = __builtin_fma(ps, z, -1.98412698298579493134e-04);
-    ps = __builtin_fma(ps, z, 8.33333333332248946124e-03);
-    ps = __builtin_fma(ps, z, -1.66666666666666324348e-01);
-    const double sn = r == 0.0 ? r : __builtin_fma(r * z, ps, r);  // sin(-0) = -0
-    double pc = __builtin_fma(-1.13596475577881948265e-11, z, 2.08757232129817482790e-09);
-    pc = __builtin_fma(pc, z, -2.75573143513906633035e-07);
-    pc = __builtin_fma(pc, z, 2.48015872894767294178e-05);
-    pc = __builtin_fma(pc, z, -1.38888888888741095749e-03);
-    pc = __builtin_fma(pc, z, 4.16666666666666019037e-02);
-    const double cs = __builtin_fma(z * z, pc, __builtin_fma(-0.5, z, 1.0));
-    const int q = ((int)k) & 3;
-    const double s = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
-    const double c = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
-    *s_out = (float)s;
-    *c_out = (float)c;
+    const float k = __builtin_rintf(th * 0.636619772f);
+    float r = __builtin_fmaf(-k, 1.5703125f, th);
+    r = __builtin_fmaf(-k, 4.837512969970703125e-4f, r);
+    r = __builtin_fmaf(-k, 7.54978995489188216e-8f, r);
+    r = k == 0.0f ? th : r;  // keeps the sign of -0
+    const float z = r * r;
+    float ps = __builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f);
+    ps = __builtin_fmaf(ps, z, -1.6666654611e-1f);
+    const float sn = r == 0.0f ? r : __builtin_fmaf(r * z, ps, r);  // sin(-0) = -0
+    float pc = __builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f);
+    pc = __builtin_fmaf(pc, z, 4.166664568298827e-2f);
+    const float hz = 0.5f * z, w = 1.0f - hz;
+    const float cs = w + (((1.0f - w) - hz) + (z * z) * pc);
+    const bool q1 = k == 1.0f, q3 = k == -1.0f, q2 = k == 2.0f || k == -2.0f;
+    *s_out = q1 ? cs : (q3 ? -cs : (q2 ? -sn : sn));
+    *c_out = q1 ? -sn : (q3 ? sn : (q2 ? -cs : cs));
 }
 
 // ----------------------------------------------------------- native RNG

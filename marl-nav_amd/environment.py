@@ -117,7 +117,8 @@ class Env(object):
                 "there is no CPU fallback")
         if self.device.index is None:
             self.device = torch.device('cuda', torch.cuda.current_device())
-        self._lib = abi.load_library()
+        # params['_lib']: a loaded alternative build (scripts/graph_time.py A/B timing)
+        self._lib = params.get('_lib') or abi.load_library()
         self.num_parallel = int(params['num_parallel'])
         self.num_agents = int(params['num_agents'])
         self.num_obstacles = int(params['num_obstacles'])

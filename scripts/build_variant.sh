@@ -1,19 +1,22 @@
 #!/bin/bash
 # Build an A/B variant of libmarlnav.so into marl-nav_amd/lib/<name>.so, from
 # the working tree with extra -D flags, or from a git revision:
-#   scripts/build_variant.sh ref HEAD             # the committed kernels
-#   scripts/build_variant.sh ntoff "" -DMARLNAV_NT_STORES=0
+#   scripts/build_variant.sh ref HEAD        # the committed kernels
+#   scripts/build_variant.sh exp "" -DSOME_TIMING_SWITCH=1
 # then: LIBS=marl-nav_amd/lib/ref.so bash scripts/cmd_ab.sh (on the GPU box)
 set -eu
-cd "$(dirname "$0")/../marl-nav_amd/csrc"
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 name=$1 rev=${2:-}
 shift $(( $# >= 2 ? 2 : 1 ))
-src=marlnav_step.hip
+src="$ROOT"
+tmp=""
 if [ -n "$rev" ]; then
-    git show "$rev:marl-nav_amd/csrc/marlnav_step.hip" > .variant_step.hip
-    src=.variant_step.hip
+    tmp=$(mktemp -d)
+    git -C "$ROOT" archive "$rev" marl-nav_amd/csrc include | tar -x -C "$tmp"
+    src="$tmp"
 fi
+cd "$src/marl-nav_amd/csrc"
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -ffp-contract=off \
-    -Wno-pass-failed "$@" "$src" marlnav_rollout.hip -o "../lib/$name.so"
-rm -f .variant_step.hip
+    -Wno-pass-failed "$@" marlnav_step.hip marlnav_rollout.hip -o "$ROOT/marl-nav_amd/lib/$name.so"
+[ -n "$tmp" ] && rm -rf "$tmp"
 echo "built marl-nav_amd/lib/$name.so"
