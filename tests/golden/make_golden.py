@@ -24,6 +24,11 @@ Fixture classes:
 * F5 ``process_rewards.npz`` - ``MAPPO._process_rewards`` (models.py:131-148)
   run unmodified (as an unbound method on a stand-in holding only the
   attributes it reads) over seeded reward/done rollouts.
+* F6 ``rollout_getdata.npz`` - ``MAPPO.get_data`` (models.py:106-129) run
+  unmodified on the reference's Env, with the actor and critic replaced by
+  stand-ins that emit a fixed seeded action stream (the policy is not on the
+  env-step path): normalised observations, raw actions, rewards, done flags
+  and the processed returns of every buffer entry, plus the episode counters.
 
 Run:  PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py
 """
@@ -266,6 +271,93 @@ def make_process_rewards(cases=((24, 96, 0.9, 21, 0.1), (7, 5, 0.99, 22, 0.3),
     return "process_rewards", rec, meta
 
 
+# ------------------------------------------------------- F6 MAPPO get_data
+class _FixedActor(torch.nn.Module):
+    """Actor stand-in: the next (P*A, 2) block of a fixed action stream as a
+    'distribution' (sample / log_prob), like models.py:113-115 expects."""
+
+    def __init__(self, stream):
+        super().__init__()
+        self.stream = stream
+        self.t = 0
+
+    def forward(self, obs):
+        a = self.stream[self.t]
+        self.t += 1
+
+        class _Dist:
+            def sample(self):
+                return a.clone()
+
+            def log_prob(self, x):
+                return torch.zeros(x.shape[0])
+        return _Dist()
+
+
+class _ZeroCritic(torch.nn.Module):
+    def forward(self, obs):
+        return torch.zeros(obs.shape[0], 1)
+
+
+def make_rollout(P=24, T=200, episode_len=40, seed=5, action_seed=31, gamma=0.9):
+    import contextlib
+    import io
+    import tempfile
+    from marlnav.models import MAPPO
+    args = cli_args(num_parallel=P, episode_len=episode_len, buffer_len=T, batch_size=T,
+                    num_total=P * T, gamma=gamma, reward_check=False, seed=seed,
+                    risk_factor=3.0, distance_factor=7.0)
+    ref_utils.set_all_seeds(seed)
+    params = ref_utils.set_params(args)
+    for k in ("env", "model"):
+        params[k]['device'] = 'cpu'
+    params['env']['init']['device'] = 'cpu'
+    params['model']['normalizer']['device'] = 'cpu'
+    params['model']['scaler']['device'] = 'cpu'
+    env = RefEnv(params['env'])
+    g = torch.Generator().manual_seed(action_seed)
+    stream = [(torch.rand(P * 3, 2, generator=g) * 2.4 - 1.2) for _ in range(T)]
+    rec = {"states0": env.states.numpy().copy(), "obstacles0": env.obstacles.numpy().copy()}
+    raw = {"reward": [], "terminated": [], "truncated": []}
+    step = env.step
+
+    def recording_step(actions):
+        out = step(actions)
+        raw["reward"].append(out[1].numpy().copy())
+        raw["terminated"].append(out[2].numpy().copy())
+        raw["truncated"].append(out[3].numpy().copy())
+        return out
+    env.step = recording_step
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                model = MAPPO(params['model'], env)
+                model.actor = _FixedActor(stream)
+                model.critic = _ZeroCritic()
+                ref_utils.set_all_seeds(seed + 1)   # the env's draws from here on
+                model.get_data()
+        finally:
+            os.chdir(cwd)
+    rec["actions"] = torch.stack(stream).numpy()
+    rec["obs_norm"] = np.stack([model.buffer[t][0].numpy() for t in range(T)])
+    rec["done"] = np.stack([model.buffer[t][5].numpy() for t in range(T)])
+    rec["returns"] = np.stack([model.buffer[t][4].numpy() for t in range(T)])
+    rec["final_obs_norm"] = model.obs.numpy()
+    for k, v in raw.items():
+        rec[k] = np.stack(v)
+    rec["mean_rew"] = np.float64(model._mean_rew.item())
+    stats = model._logs['epi_stats']
+    meta = {"kind": "F6", "num_parallel": P, "buffer_len": T, "episode_len": episode_len,
+            "seed": seed, "reseed": seed + 1, "action_seed": action_seed, "gamma": gamma,
+            "risk_factor": 3.0, "distance_factor": 7.0,
+            "action_stream": "torch.rand(P*3, 2, Generator(action_seed)) * 2.4 - 1.2 per step",
+            "num_trunc": stats['trunc'][-1], "num_col": stats['col'][-1],
+            "num_tar": stats['tar'][-1], "returns_dtype": str(model.buffer[0][4].dtype)}
+    return "rollout_getdata", rec, meta
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*", help="fixture names to (re)generate")
@@ -284,6 +376,7 @@ def main():
         make_trace("trace_mock1", 1, 1000, None),
         make_triangle_rng(),
         make_process_rewards(),
+        make_rollout(),
     ] if not cli.only else [JOBS[n]() for n in cli.only]
     mpath = os.path.join(HERE, "MANIFEST.json")
     manifest = {"torch": torch.__version__, "numpy": np.__version__,
@@ -302,7 +395,8 @@ def main():
         json.dump(manifest, fh, indent=1, sort_keys=True)
 
 
-JOBS = {"process_rewards": make_process_rewards, "triangle_rng": make_triangle_rng}
+JOBS = {"process_rewards": make_process_rewards, "triangle_rng": make_triangle_rng,
+        "rollout_getdata": make_rollout}
 
 
 if __name__ == "__main__":

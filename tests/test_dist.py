@@ -101,3 +101,28 @@ def test_strong_slices_partition(pkg, total, world):
     assert all(got[i][0] + got[i][1] == got[i + 1][0] for i in range(world - 1))
     assert max(n for _, n in got) - min(n for _, n in got) <= 1
     assert pkg.shard.weak_slice(3, 65536) == (3 * 65536, 65536)
+
+
+def test_bench_self_launches_n_ranks(monkeypatch):
+    """`python bench.py --gpus N` outside torch.distributed.run starts the
+    launcher with N ranks on 127.0.0.1 (before any GPU call) and returns its
+    status; it never times one GPU and reports n_gpus 1 for --gpus N."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    calls = []
+    monkeypatch.setattr(bench.subprocess, "call", lambda cmd: calls.append(cmd) or 7)
+    for k in ("WORLD_SIZE", "LOCAL_RANK", "RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "20", "--warmup", "5"])
+    assert bench.main() == 7
+    (cmd,) = calls
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=4" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-6:] == ["--gpus", "4", "--steps", "20", "--warmup", "5"]
+    # under the launcher, a rank count that disagrees with --gpus is an error
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    with pytest.raises(SystemExit):
+        bench.main()

@@ -901,3 +901,52 @@ def test_configs4_sharded_slices_equal_one_batch_and_oracle(pkg):
     tot = np.sum([[e._num_trunc, e._num_col, e._num_tar] for e in shards], axis=0)
     assert tot.tolist() == [full._num_trunc, full._num_col, full._num_tar]
     assert tot[0] > 0 and tot[1] > 0
+
+
+def test_mappo_get_data_rollout_matches_reference(pkg):
+    """F6: the reference's MAPPO.get_data loop (models.py:106-129: normalise
+    observations, step with up-scaled policy actions, keep obs / actions /
+    log-probs / values / rewards / done, then _process_rewards) run on the
+    drop-in Env with the fused ObsNormalizer and ActionScaler and the device
+    RolloutBuffer, reference-RNG mode: 200 steps of normalised observations,
+    rewards and done flags and the processed returns against the reference's
+    (trajectory tolerances: tests/conftest.py assert_traj_obs_close)."""
+    import math
+    from conftest import assert_traj_obs_close
+    m, z = meta("rollout_getdata"), golden("rollout_getdata")
+    P, A, O, T = m["num_parallel"], 3, 3, m["buffer_len"]
+    args = cli_args(num_parallel=P, episode_len=m["episode_len"], risk_factor=m["risk_factor"],
+                    distance_factor=m["distance_factor"], buffer_len=T, gamma=m["gamma"])
+    nrm = pkg.ObsNormalizer(pkg.set_normalizer_params(args, DEV))
+    scl = pkg.ActionScaler(pkg.set_scaler_params(args, DEV))
+    pkg.set_all_seeds(m["seed"])
+    params = pkg.set_env_params(args, DEV)
+    params["init"] = dict(params["init"], noise_device="cpu")
+    params["rng"] = "reference"
+    env = pkg.Env(params)
+    np.testing.assert_array_equal(np_(env.states), z["states0"])
+    env.attach_normalizer(nrm)
+    env.attach_action_scaler(scl)
+    pkg.set_all_seeds(m["reseed"])
+    obs_n = nrm(env.observations())
+    buf = pkg.rollout.RolloutBuffer(T)
+    for t in range(T):
+        assert_traj_obs_close(np_(obs_n), z["obs_norm"][t], A, O, angle_scale=math.pi,
+                              what=f"obs_norm {t}")
+        raw = torch.from_numpy(z["actions"][t]).to(DEV)
+        obs, rew, term, trunc = env.step(raw.view(P, A, 2))       # scaled in the kernel
+        done = torch.logical_or(term, trunc)
+        np.testing.assert_array_equal(np_(done), z["done"][t], f"done {t}")
+        assert_vec_close(np_(rew), z["reward"][t], atol=1e-4, what=f"reward {t}")
+        buf.add(obs_n, raw, torch.zeros(P * A, device=DEV), torch.zeros(P, 1, device=DEV),
+                rew, done)
+        obs_n = nrm(obs)
+        assert obs_n is obs._normalized                             # the fused copy
+    assert_traj_obs_close(np_(obs_n), z["final_obs_norm"], A, O, angle_scale=math.pi,
+                          what="final obs")
+    mean = buf.process_rewards(m["gamma"])
+    ret = np.stack([np_(e[4]) for e in buf.entries()])
+    np.testing.assert_allclose(ret, z["returns"], rtol=1e-5, atol=1e-6)
+    assert abs(float(mean) - float(z["mean_rew"])) <= 1e-5 * abs(float(z["mean_rew"]))
+    assert (env._num_trunc, env._num_col, env._num_tar) == (m["num_trunc"], m["num_col"],
+                                                            m["num_tar"])

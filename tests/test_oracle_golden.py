@@ -1,12 +1,14 @@
 """Pin the C oracle (oracle/marlnav_oracle.c) and the host samplers to the
 reference: every golden vector in tests/golden/ was produced by the
 reference's own Env (tests/golden/make_golden.py). CPU only."""
+import math
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import (OBS_FIELDS, assert_obs_close, assert_states_close, assert_vec_close,
-                      cli_args, env_values, golden, meta)
+from conftest import (OBS_FIELDS, assert_obs_close, assert_states_close, assert_traj_obs_close,
+                      assert_vec_close, cli_args, env_values, golden, meta)
 
 import oracle as orc
 
@@ -274,3 +276,73 @@ def test_oracle_blend_matches_reference_expression_on_non_finite_values(A, O, mk
     # the cases above really are exercised: NaN where the reference has NaN
     assert np.isnan(o["states"][0, 0, 0]) and np.isnan(o["states"][1, 0, 3])
     assert np.isnan(o["obstacles"][3, 0, 0]) and o["states"][8, 2 % A, 0] == inf
+
+
+def _rollout_setup(pkg, device):
+    """Params, normaliser and scaler of the F6 rollout (MAPPO.get_data,
+    models.py:106-129) and the fixed action stream."""
+    m, z = meta("rollout_getdata"), golden("rollout_getdata")
+    args = cli_args(num_parallel=m["num_parallel"], episode_len=m["episode_len"],
+                    risk_factor=m["risk_factor"], distance_factor=m["distance_factor"],
+                    buffer_len=m["buffer_len"], gamma=m["gamma"])
+    nrm = pkg.ObsNormalizer(pkg.set_normalizer_params(args, device))
+    scl = pkg.ActionScaler(pkg.set_scaler_params(args, device))
+    return m, z, args, nrm, scl
+
+
+def _fields(obs, A, O):
+    """A packed (P, A, D) oracle observation as the six Observations fields."""
+    return tuple(torch.from_numpy(np.ascontiguousarray(f)) for f in orc.split_obs(obs, A, O))
+
+
+def test_oracle_replays_mappo_get_data(pkg):
+    """F6: MAPPO.get_data of the reference (models.py:106-129) replayed with
+    the oracle step, this package's host init sampler (reference RNG,
+    utils.py:375-398), ObsNormalizer, ActionScaler and the oracle's
+    discounted returns: normalised observations, rewards and done flags of
+    all 200 steps and the processed returns, against the reference's."""
+    m, z, args, nrm, scl = _rollout_setup(pkg, "cpu")
+    P, A, O = m["num_parallel"], 3, 3
+    pkg.set_all_seeds(m["seed"])
+    params = pkg.set_env_params(args, "cpu")
+    init = pkg.init_sampler(dict(params["init"], num_agents=A))
+    st, ob, tg = (t.numpy().copy() for t in init())      # Env.__init__ draw
+    np.testing.assert_array_equal(st, z["states0"])
+    np.testing.assert_array_equal(ob, z["obstacles0"])
+    import marlnav_amd.environment as envmod
+    pr = envmod.make_cparams({"min_speed": 3.0, "max_speed": 10.0, "min_accel": -0.5,
+                              "max_accel": 0.5, "_risk_factor": m["risk_factor"],
+                              "_distance_factor": m["distance_factor"],
+                              "_heading_factor": 500.0, "_target_factor": 500.0,
+                              "_soft_factor": 500.0, "_bond_factor": 10.0,
+                              "episode_len": m["episode_len"]})
+    dm = orc.make_dims(P, A, O)
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    pkg.set_all_seeds(m["reseed"])
+    obs = orc.observe(dm, st, ob, tg, params=pr)
+    rewards, dones = [], []
+    worst = 0.0
+    for t in range(m["buffer_len"]):
+        on = nrm(_fields(obs, A, O)).numpy()
+        worst = max(worst, float(np.abs(on - z["obs_norm"][t]).max()))
+        assert_traj_obs_close(on, z["obs_norm"][t], A, O, angle_scale=math.pi,
+                              what=f"obs_norm {t}")
+        acts = scl(torch.from_numpy(z["actions"][t]).view(P, A, 2)).numpy()
+        fresh = tuple(x.numpy() for x in init())          # environment.py:78
+        o = orc.step(dm, pr, st, ob, tg, sn, te, acts, fresh=fresh)
+        done = np.logical_or(o["terminated"], o["truncated"])
+        np.testing.assert_array_equal(done, z["done"][t], f"done {t}")
+        # a reward is a sum of terms of magnitude ~500 that can cancel to ~0:
+        # an ulp of a term (3e-5) is the absolute floor
+        assert_vec_close(o["reward"], z["reward"][t], atol=1e-4, what=f"reward {t}")
+        rewards.append(o["reward"])
+        dones.append(done)
+        st, ob, tg, sn, te, obs = (o[x] for x in ("states", "obstacles", "target", "step_num",
+                                                  "terminates", "obs"))
+    assert_traj_obs_close(nrm(_fields(obs, A, O)).numpy(), z["final_obs_norm"], A, O,
+                          angle_scale=math.pi, what="final obs")
+    print("worst normalised-obs deviation", worst)
+    ret, (mean, std) = orc.discounted_returns(np.stack(rewards), np.stack(dones), m["gamma"])
+    np.testing.assert_allclose(ret, z["returns"], rtol=1e-5, atol=1e-6)
+    assert abs(mean - float(z["mean_rew"])) <= 1e-5 * abs(float(z["mean_rew"]))
