@@ -768,133 +768,6 @@ __device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
     return out;
 }
 
-// observe_row_own's FAST path written stage by stage across the row's
-// 1 + O + (A - 1) pairs (all differences, then all squared distances, all
-// square roots, ...): the same operations on the same values, so the same
-// bits, in an order that keeps every pair's dependent chain in flight
-// together (the pairs are independent; one-pair-at-a-time code leaves the
-// SIMD waiting on each chain's latency).
-template <int A, int O, bool TERMS>
-__device__ __forceinline__ RowOut observe_row_staged(const float *__restrict__ sts,
-                                                     const float *__restrict__ obe,
-                                                     const float *__restrict__ tge, int a,
-                                                     float ox, float oy, float dirx, float diry,
-                                                     float *row, const MarlnavParams &pr,
-                                                     bool &ok)
-{
-    constexpr int NP = 1 + O + (A - 1);
-    const float cap = pr.cap_distance;
-    float px[NP], py[NP];
-    px[0] = tge[0];
-    py[0] = tge[1];
-#pragma unroll
-    for (int j = 0; j < O; ++j) {
-        px[1 + j] = obe[2 * j];
-        py[1 + j] = obe[2 * j + 1];
-    }
-#pragma unroll
-    for (int j = 0; j < A - 1; ++j) {
-        const int m = j + (j >= a ? 1 : 0);
-        px[1 + O + j] = sts[5 * m];
-        py[1 + O + j] = sts[5 * m + 1];
-    }
-    float dx[NP], dy[NP], d[NP], nx[NP], ny[NP], dot[NP], ang[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        dx[j] = px[j] - ox;
-        dy[j] = py[j] - oy;
-    }
-#pragma unroll
-    for (int j = 0; j < NP; ++j) d[j] = __builtin_fmaf(dy[j], dy[j], dx[j] * dx[j]);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) d[j] = sqrt_fast(d[j], ok);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const float den = __builtin_amdgcn_fmed3f(d[j], 1e-12f, __builtin_inff());
-        div2_fast(dx[j], dy[j], den, &nx[j], &ny[j], ok);
-    }
-#pragma unroll
-    for (int j = 0; j < NP; ++j)
-        dot[j] = __builtin_amdgcn_fmed3f(dirx * nx[j] + diry * ny[j], -1.0f, 1.0f);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) ang[j] = acosf(dot[j]);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const float orth_x = nx[j] - dot[j] * dirx;
-        const float a2 = (orth_x > 0.0f ? -1.0f : 1.0f) * ang[j];
-        ang[j] = d[j] < cap ? 0.0f : a2;
-    }
-    row[0] = ang[0];
-    row[1] = d[0];
-#pragma unroll
-    for (int j = 0; j < O; ++j) {
-        row[2 + j] = ang[1 + j];
-        row[2 + O + j] = d[1 + j];
-    }
-#pragma unroll
-    for (int j = 0; j < A - 1; ++j) {
-        row[2 + 2 * O + j] = ang[1 + O + j];
-        row[2 + 2 * O + (A - 1) + j] = d[1 + O + j];
-    }
-    RowOut out{0.0f, 0.0f, 0u};
-    if (TERMS) {
-        bool ob_risk = false, ob_col = false, ag_risk = false, ag_col = false;
-        float band = 0.0f;
-#pragma unroll
-        for (int j = 0; j < O; ++j) {
-            ob_risk |= d[1 + j] < pr.ob_risk_dist;
-            ob_col |= d[1 + j] < pr.ob_coll_dist;
-        }
-#pragma unroll
-        for (int j = 0; j < A - 1; ++j) {
-            const float dj = d[1 + O + j];
-            ag_risk |= dj < pr.ag_risk_dist;
-            ag_col |= dj < pr.ag_coll_dist;
-            band += (pr.agents_min_d < dj && dj < pr.agents_max_d) ? 1.0f : 0.0f;
-        }
-        const float td = d[0], ta = ang[0];
-        const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
-        const float ideal = pr.ideal_dist, sharp = pr.bond_sharpness;
-        const float bandc = band < pr.max_at_prop_d ? band : pr.max_at_prop_d;
-        float dsc, soft, bondm;
-        if (pr.flags & kTermsFastFlag) {
-            const DivC d_mapd = make_divc(pr.max_at_prop_d, ok);
-            const DivC d_init = make_divc(pr.init_dist, ok);
-            const DivC d_sharp = make_divc(sharp, ok);
-            dsc = div_c(bandc, d_mapd, ok);
-            soft = -1.0f * div_c(td, d_init, ok);
-            const float bond = torch_row_sum_r<A - 1>(d + 1 + O, [&](float dj) {
-                const float sd = div_c(dj - ideal, d_sharp, ok);
-                return recip_fast(1.0f + sd * sd, ok);
-            });
-            bondm = bond / (float)(A - 1);
-        } else {
-            dsc = bandc / pr.max_at_prop_d;
-            soft = -1.0f * (td / pr.init_dist);
-            const float bond = torch_row_sum_r<A - 1>(d + 1 + O, [ideal, sharp](float dj) {
-                const float sd = (dj - ideal) / sharp;
-                return 1.0f / (1.0f + sd * sd);
-            });
-            bondm = bond / (float)(A - 1);
-        }
-        const float risk = (ob_risk || ag_risk) ? 1.0f : 0.0f;
-        float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
-        float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
-        rm = rm + pr.distance_factor * dsc;
-        rh = rh + pr.distance_factor * dsc;
-        rm = rm + pr.soft_factor * soft;
-        rh = rh + pr.soft_factor * soft;
-        rm = rm + pr.bond_factor * bondm;
-        rh = rh + pr.bond_factor * bondm;
-        rm = rm - pr.risk_factor * risk;
-        rh = rh - pr.risk_factor * risk;
-        out.r_miss = rm;
-        out.r_hit = rh;
-        out.flags = ((ob_col || ag_col) ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u);
-    }
-    return out;
-}
-
 template <int A, int O, bool TERMS, bool FAST>
 __device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts,
                                                    const float *__restrict__ obe,

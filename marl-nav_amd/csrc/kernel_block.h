@@ -18,10 +18,7 @@
 // register-row stores at a 48-byte lane stride touch 24).
 template <int A, int O>
 struct BlockPlan {
-#ifndef EXP_E
-#define EXP_E 64
-#endif
-    static constexpr int E = EXP_E, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
+    static constexpr int E = 64, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
     static constexpr int NT = 64 * A;                      // threads per block
     static constexpr int ST = 0;                           // (R, 5)
     static constexpr int ACT = (ST + R * 5 + 3) & ~3;      // (R, 2)
@@ -100,15 +97,6 @@ __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float
 // (moved states start streaming out) | observe into LDS rows | rows stream
 // out while wave 0 runs the per-env phase | re-init, re-observe and re-store
 // the finished envs only (none in most blocks).
-#ifndef EXP_OBS_OWN
-#define OBSFN observe_row_staged
-#else
-template <int A, int O, bool T>
-__device__ __forceinline__ RowOut obs_own_fast(const float *a, const float *b, const float *c, int w,
-    float ox, float oy, float dx, float dy, float *row, const MarlnavParams &pr, bool &ok)
-{ return observe_row_own<A, O, T, true>(a, b, c, w, ox, oy, dx, dy, row, pr, ok); }
-#define OBSFN obs_own_fast
-#endif
 template <int A, int O, bool OBS_ONLY, bool NOISY>
 __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
 {
@@ -246,7 +234,7 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
         RowOut ro;
         bool unused = true;
         if (__builtin_expect(fast, 1))
-            ro = OBSFN<A, O, !OBS_ONLY>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
+            ro = observe_row_own<A, O, !OBS_ONLY, true>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
                                                         lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
                                                         rowv, pr, unused);
         else
