@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MARLNAV_ABI_VERSION 2
+#define MARLNAV_ABI_VERSION 3
 
 /* error codes */
 #define MARLNAV_OK 0
@@ -123,6 +123,12 @@ typedef struct MarlnavStepBuffers {
     float *obs_norm;         /* (P, A, D)                                  */
     const float *norm_mean;  /* (D,)                                       */
     const float *norm_scale; /* (D,)                                       */
+    /* optional observation template of a native fresh env (NULL: computed
+     * in full): marlnav_formation_obs() of `formation`. Finished envs whose
+     * agent rows and target re-initialise to the formation exactly (every
+     * old value finite) take their target and agent-agent pairs from it and
+     * compute only the agent-obstacle pairs. */
+    const float *formation_obs; /* (A, A, 2)                               */
 } MarlnavStepBuffers;
 
 /* Env.step(actions) - environment.py:92-107 (with _move_agents :113-137,
@@ -146,6 +152,16 @@ int marlnav_reinit_all(const MarlnavDims *dims, const MarlnavParams *params,
                        const float *formation, float *states,
                        float *obstacles, float *target, uint64_t step_idx,
                        void *stream);
+
+/* Observation template of the native re-init's fresh env (the
+ * TriangleIntitializer formation, utils.py:350-368, observed as in
+ * environment.py:139-166): out[(a*A + m)*2 + {0, 1}] = (bearing before the
+ * cap of environment.py:172-177, distance) of agent a to pair m, m = 0 the
+ * target, m >= 1 the other agents in ascending order skipping a. The same
+ * fp32 arithmetic as the step kernels' observation. formation: 5A + 2
+ * floats (as MarlnavStepBuffers.formation); out: 2*A*A floats. */
+int marlnav_formation_obs(const MarlnavDims *dims, const float *formation, float *out,
+                          void *stream);
 
 /* Number of uint64 partial-sum slots per counter row for these dims. */
 int64_t marlnav_counter_slots(const MarlnavDims *dims);

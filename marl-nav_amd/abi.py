@@ -11,7 +11,7 @@ fallback: if the library is missing or fails to load, ``load_library`` raises.
 import ctypes
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 FRESH_STATES_FROM_MOVED = 0x1
 NOISY_AGENTS = 0x2
@@ -53,14 +53,14 @@ STEP_BUFFER_FIELDS = (
     "states", "obstacles", "target", "step_num", "terminates", "actions",
     "fresh_states", "fresh_obstacles", "fresh_target", "formation", "obs",
     "reward", "terminated", "truncated", "counters", "obs_norm", "norm_mean",
-    "norm_scale")
+    "norm_scale", "formation_obs")
 
 
 class MarlnavStepBuffers(ctypes.Structure):
     _fields_ = [(n, _P) for n in STEP_BUFFER_FIELDS]
 
 
-EXPORTS = ("marlnav_step", "marlnav_observe", "marlnav_reinit_all",
+EXPORTS = ("marlnav_step", "marlnav_observe", "marlnav_reinit_all", "marlnav_formation_obs",
            "marlnav_counter_slots", "marlnav_counters_total",
            "marlnav_returns_work_size", "marlnav_discounted_returns",
            "marlnav_last_error", "marlnav_abi_version",
@@ -81,6 +81,8 @@ def _declare(lib):
     lib.marlnav_observe.restype = c.c_int
     lib.marlnav_reinit_all.argtypes = [dims_p, par_p, _P, _P, _P, _P, c.c_uint64, _P]
     lib.marlnav_reinit_all.restype = c.c_int
+    lib.marlnav_formation_obs.argtypes = [dims_p, _P, _P, _P]
+    lib.marlnav_formation_obs.restype = c.c_int
     lib.marlnav_counter_slots.argtypes = [dims_p]
     lib.marlnav_counter_slots.restype = c.c_int64
     lib.marlnav_counters_total.argtypes = [dims_p, _P, _P, _P]

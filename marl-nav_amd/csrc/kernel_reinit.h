@@ -87,6 +87,54 @@ __device__ __forceinline__ void reobs_block(const Envs &ev, const List &list, in
     }
 }
 
+// reobs_block for re-initialised envs that all equal the native fresh env
+// in their agent rows and target (reinit_block found no `unclean` env): the
+// target and agent-agent pairs come from the formation template `tpl`
+// (marlnav_formation_obs: raw bearing, distance), only the agent-obstacle
+// pairs are computed. Item (env, agent, obstacle j) also writes the template
+// pairs m = j, j + O, ... < A of its agent row.
+template <int A, int O, class Envs, class List>
+__device__ __forceinline__ void reobs_block_tpl(const Envs &ev, const List &list, int nfin,
+                                                float cap, const float2 *__restrict__ tpl,
+                                                int tid, int nt)
+{
+    const int nw = nfin * A * O;
+    for (int base = 0; base < nw; base += nt) {
+        const int w = base + tid;
+        const bool on = w < nw;
+        const int wc = on ? w : 0;
+        const int fe = wc / (A * O), rem = wc - fe * (A * O);
+        const int ag = rem / O, j = rem - ag * O;
+        const int c = list[fe];
+        const float *s = ev.state(c) + 5 * ag;
+        const float ox = s[0], oy = s[1], dx = s[2], dy = s[3];
+        const float *pt = ev.obst(c) + 2 * j;
+        const float px = pt[0], py = pt[1];
+        const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+        bool unused = true;
+        float d, ang;
+        if (__ballot(on && !cok) == 0ull) {
+            d = pair_dist<true>(ox, oy, px, py, unused);
+            ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+        } else {
+            d = pair_dist<false>(ox, oy, px, py, unused);
+            ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+        }
+        if (on) {
+            float *o = ev.row(c, ag);
+            o[2 + j] = ang;
+            o[2 + O + j] = d;
+            for (int m = j; m < A; m += O) {
+                const float2 t = tpl[ag * A + m];
+                const int sa = m == 0 ? 0 : 2 + 2 * O + (m - 1);
+                const int sd = m == 0 ? 1 : 2 + 2 * O + (A - 1) + (m - 1);
+                o[sa] = t.y < cap ? 0.0f : t.x;  // the cap (environment.py:172-177)
+                o[sd] = t.y;
+            }
+        }
+    }
+}
+
 template <int D>
 __device__ __forceinline__ void lds_row_write(float *dst, const float *row)
 {
@@ -110,9 +158,14 @@ __device__ __forceinline__ void lds_row_write(float *dst, const float *row)
 // or one Philox block of two obstacles (native; the same draws as
 // native_fresh_env). Writes the LDS state and the global obstacles / target;
 // the agent rows go out with the final stores.
+// `unclean` (optional, native re-init): set to 1 when a finished env's
+// blended agent coordinates or target differ from the formation's bits (a
+// non-finite old value blends to NaN), i.e. when the formation template
+// (reobs_block_tpl) does not describe the re-initialised env.
 template <int A, int O, class Envs, class List>
 __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const float *form,
-                                             const List &list, int nfin, int tid, int nt)
+                                             const List &list, int nfin, int tid, int nt,
+                                             int *unclean = nullptr)
 {
     float *gob = kl->a.b.obstacles;
     float *gtg = kl->a.b.target;
@@ -155,13 +208,17 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
         const int64_t e = ev.env(c);
         if (kk < 5 * A) {
             float *d = ev.state(c) + kk;
-            *d = blend_in(*d, form[kk]);
+            const float v = blend_in(*d, form[kk]);
+            *d = v;
+            if (unclean && kk % 5 < 4 && __float_as_uint(v) != __float_as_uint(form[kk]))
+                *unclean = 1;
         } else if (kk < 5 * A + 2) {
             const int j = kk - 5 * A;
             float *d = ev.targ(c) + j;
             const float v = blend_in(*d, form[kk]);
             *d = v;
             gtg[2 * e + j] = v;
+            if (unclean && __float_as_uint(v) != __float_as_uint(form[kk])) *unclean = 1;
         } else {
             const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
             const uint64_t gid = (uint64_t)(eoff + e);

@@ -77,6 +77,12 @@ struct SplitFinList {
 template <int A, int O>
 constexpr bool kSplitSpread = A * (1 + O + (A - 1)) >= 32;
 
+// Spread re-init of many-obstacle shapes (O > 8: reinit_block, then the
+// re-observation) with the formation and its observation template staged in
+// LDS (kernel_reinit.h: reobs_block_tpl).
+template <int A, int O>
+constexpr bool kSplitTpl = kSplitSpread<A, O> && O > 8;
+
 template <int A, int O, int LPR>
 struct SplitPlan {
     static constexpr int EPW = 64 / LPR / A;  // envs per wave
@@ -94,8 +100,14 @@ struct SplitPlan {
     static constexpr int BOND = (OBS + R * DP + 3) & ~3;   // (R, A-1)
     static constexpr int RED = (BOND + R * (A - 1) + 3) & ~3;  // (R, 4)
     static constexpr int FLOATS = RED + 4 * R;
-    // after the waves' regions: finished-env counts and slots of the workgroup
-    static constexpr int BLK = (kWavesPerBlock * (1 + EPW) + 3) & ~3;
+    // formation (5A + 2 floats) and its observation template (2A^2 floats),
+    // staged for the spread re-init of kSplitTpl shapes
+    static constexpr int NF = 5 * A + 2, NCP = NF + 2 * A * A;
+    // after the waves' regions: finished-env counts and slots of the
+    // workgroup, the `unclean` word (reinit_block), then (kSplitTpl) the
+    // formation and template at FTP
+    static constexpr int FTP = (kWavesPerBlock * (1 + EPW) + 1 + 3) & ~3;
+    static constexpr int BLK = FTP + (kSplitTpl<A, O> ? NCP : 0);
     static_assert(EPW >= 1, "an env's rows must fit one wave");
 };
 
@@ -247,7 +259,10 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
 }
 
 template <int A, int O, int LPR, bool OBS_ONLY, bool NOISY>
-__global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
+// (min 4 waves per SIMD: keeps the max-ilp scheduler (Makefile) within the
+// 128 VGPRs of the 4-waves-per-SIMD grids; unbounded it takes 178 at A16/O32
+// and halves occupancy)
+__global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
 {
     using SP = SplitPlan<A, O, LPR>;
     constexpr int EPW = SP::EPW, R = SP::R, D = SP::D;
@@ -408,6 +423,26 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
     }
     STAMP(3);
 
+    // formation + template (kSplitTpl, native re-init) into registers now,
+    // so their load latency hides behind the per-env phase; a block that
+    // finds finished envs parks them in LDS for reinit_block /
+    // reobs_block_tpl
+    constexpr int KCP = (SP::NCP + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock);
+    float cp[KCP];
+    bool tpl_on = false;
+    if constexpr (kSplitTpl<A, O> && !NOISY && !OBS_ONLY) {
+        KArgsK *kl = kargs_late();
+        const float *cfo = kl->a.b.formation, *ctp = kl->a.b.formation_obs;
+        tpl_on = ctp && !kl->a.b.fresh_states;
+        if (tpl_on) {
+#pragma unroll
+            for (int k2 = 0; k2 < KCP; ++k2) {
+                const int idx = (int)threadIdx.x + k2 * 64 * kWavesPerBlock;
+                if (idx < SP::NCP) cp[k2] = idx < SP::NF ? cfo[idx] : ctp[idx - SP::NF];
+            }
+        }
+    }
+
     if (!OBS_ONLY) {
         wave_sync();
         // ---- per-env reductions, terminal logic, masked re-init
@@ -493,6 +528,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
             // on its own lanes (the straggler that set the kernel's end)
             int *bcnt = reinterpret_cast<int *>(lds + kWavesPerBlock * SP::FLOATS);
             int *bslot = bcnt + kWavesPerBlock;
+            int *unclean = bslot + kWavesPerBlock * EPW;
+            if (threadIdx.x == 0) *unclean = 0;
             if (fin)
                 bslot[wib * EPW + (int)__builtin_amdgcn_mbcnt_hi(
                                       (unsigned)(finmask >> 32),
@@ -518,6 +555,30 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) split_kernel(KArgs k)
                 if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
                     reinit_reobs_native<A, O>(kl, ev, kl->a.b.formation, list, nfin,
                                               pr.cap_distance, tid, nt);
+                } else if (kSplitTpl<A, O> && tpl_on) {
+                    // formation + template to LDS (from the registers when all
+                    // the block's waves are live, else straight from global)
+                    float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
+                    if (live == kWavesPerBlock) {
+#pragma unroll
+                        for (int k2 = 0; k2 < KCP; ++k2) {
+                            const int idx = tid + k2 * 64 * kWavesPerBlock;
+                            if (idx < SP::NCP) ftp[idx] = cp[k2];
+                        }
+                    } else {
+                        for (int idx = tid; idx < SP::NCP; idx += nt)
+                            ftp[idx] = idx < SP::NF ? kl->a.b.formation[idx]
+                                                    : kl->a.b.formation_obs[idx - SP::NF];
+                    }
+                    __syncthreads();
+                    reinit_block<A, O>(kl, ev, ftp, list, nfin, tid, nt, unclean);
+                    __syncthreads();
+                    if (*unclean == 0)
+                        reobs_block_tpl<A, O>(ev, list, nfin, pr.cap_distance,
+                                              reinterpret_cast<const float2 *>(ftp + SP::NF),
+                                              tid, nt);
+                    else
+                        reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
                 } else {
                     if (!NOISY) {
                         reinit_block<A, O>(kl, ev, kl->a.b.formation, list, nfin, tid, nt);

@@ -93,6 +93,28 @@ __global__ void reinit_all_kernel(int64_t P, int A, int S, int64_t env_offset, u
                                 states + e * A * 5, obstacles + e * S * 2, target + 2 * e);
 }
 
+// marlnav_formation_obs: one thread per (agent a, pair m) of the formation;
+// the IEEE pair math, equal to every kernel's (the short sequences agree
+// with it wherever they run); cap 0 leaves the bearing uncapped
+__global__ void formation_obs_kernel(int A, const float *__restrict__ form, float *__restrict__ out)
+{
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= A * A) return;
+    const int a = i / A, m = i - a * A;
+    const float ox = form[5 * a], oy = form[5 * a + 1];
+    const float dx = form[5 * a + 2], dy = form[5 * a + 3];
+    float px = form[5 * A], py = form[5 * A + 1];
+    if (m > 0) {
+        const int k = (m - 1) + (m - 1 >= a ? 1 : 0);
+        px = form[5 * k];
+        py = form[5 * k + 1];
+    }
+    bool unused = true;
+    const float d = pair_dist<false>(ox, oy, px, py, unused);
+    out[2 * i] = pair_angle<false>(ox, oy, px, py, dx, dy, d, 0.0f, unused);
+    out[2 * i + 1] = d;
+}
+
 __global__ void counters_total_kernel(const uint64_t *__restrict__ c, int64_t slots,
                                       uint64_t *out3)
 {
@@ -497,6 +519,20 @@ int marlnav_reinit_all(const MarlnavDims *d, const MarlnavParams *pr, const floa
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(MARLNAV_ELAUNCH, "marlnav_reinit_all: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int marlnav_formation_obs(const MarlnavDims *d, const float *formation, float *out,
+                          void *stream)
+{
+    if (int rc = validate(d)) return rc;
+    if (!formation || !out) return fail(MARLNAV_EINVAL, "formation/out is NULL");
+    const int n = d->num_agents * d->num_agents;
+    hipLaunchKernelGGL(formation_obs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d->num_agents, formation, out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(MARLNAV_ELAUNCH, "marlnav_formation_obs: %s", hipGetErrorString(e));
     return 0;
 }
 

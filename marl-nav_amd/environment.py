@@ -168,6 +168,7 @@ class Env(object):
         self._dims = abi.MarlnavDims()
         self._cparams = abi.MarlnavParams()
         self._formation = None
+        self._formation_obs = None
         if is_triangle:
             smp = self._init_sampler
             form = torch.cat([smp.formation.reshape(-1), smp.target_point.reshape(-1)])
@@ -180,6 +181,12 @@ class Env(object):
             self._set_state_buffers(torch.empty(P, A, 5, device=self.device),
                                     torch.empty(P, S, 2, device=self.device),
                                     torch.empty(P, 1, 2, device=self.device))
+            # the fresh env's target and agent-agent pairs, observed once
+            # (re-observations of finished envs then compute only obstacles)
+            self._formation_obs = torch.empty(A, A, 2, device=self.device)
+            abi.check(self._lib.marlnav_formation_obs(
+                ctypes.byref(self._dims), self._formation.data_ptr(),
+                self._formation_obs.data_ptr(), _stream_handle(self.device)), self._lib)
             self._sync_params()
             abi.check(self._lib.marlnav_reinit_all(
                 ctypes.byref(self._dims), ctypes.byref(self._cparams),
@@ -227,6 +234,8 @@ class Env(object):
         b.terminates = self.__dict__['_terminates_t'].data_ptr()
         b.counters = self._counters.data_ptr()
         b.formation = self._formation.data_ptr() if self._formation is not None else None
+        fo = self.__dict__.get('_formation_obs')
+        b.formation_obs = fo.data_ptr() if fo is not None else None
         if self._obs_norm_buffers is not None:
             b.norm_mean = self._obs_norm_buffers[0].data_ptr()
             b.norm_scale = self._obs_norm_buffers[1].data_ptr()

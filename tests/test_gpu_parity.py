@@ -803,13 +803,17 @@ def test_reference_rng_non_finite_fresh_candidates(pkg, P, A, O):
                    acts, fresh_list=fresh_list, where=f"P{P} A{A} O{O}")
 
 
+@pytest.mark.parametrize("shape", [(5000 + 3, 3, 3, 9), (600, 16, 32, 2)])
 @pytest.mark.parametrize("cap", [50.0, 0.0, 1e6])
-def test_cap_distance_reaches_step_and_observe(pkg, cap):
+def test_cap_distance_reaches_step_and_observe(pkg, cap, shape):
     """env._cap_distance (environment.py:65) caps the angles in step AND in
-    observations()/reset() (environment.py:172-177), like the reference."""
-    P, A, O = 5000 + 3, 3, 3
+    observations()/reset() (environment.py:172-177), like the reference;
+    with 2-step episodes also in the re-observation of re-initialised envs
+    (at A16/O32 through the formation template, whose bearings are stored
+    uncapped)."""
+    P, A, O, ep = shape
     g = torch.Generator().manual_seed(7)
-    env = make_env(pkg, P, A, O, episode_len=9, seed=4)
+    env = make_env(pkg, P, A, O, episode_len=ep, seed=4)
     env._cap_distance = cap
     dm, pr = oracle_params(env)
     assert abs(pr.cap_distance - cap) <= 1e-6 * max(cap, 1.0)
