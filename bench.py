@@ -110,6 +110,7 @@ def kernel_time_us(env, actions, n=25, replays=12):
     replays of a hipGraph holding n back-to-back Env.step launches of ``env``
     (each interval includes the graph's inter-kernel boundary, as a
     back-to-back rocprofv3 kernel duration does). Returns (mean, median)."""
+    env.allow_graph_capture = True  # replays repeat the captured re-init draws: timing only
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):

@@ -91,6 +91,7 @@ struct Engine {
     int64_t act_shape[3];
     int fast_ok;                  // native re-init, default sampler, params in sync
     int write_norm;               // sets carry a normaliser output
+    int allow_capture;            // launches under stream capture accepted (timing)
     unsigned long long step_idx;  // native RNG step counter (environment.py:92 call count + 1)
     unsigned long long steps_done;
     std::vector<OutSet *> *pool;
@@ -235,6 +236,16 @@ PyObject *do_launch(Engine *e, const void *actions, const MarlnavStepBuffers *fr
         cap = hipStreamCaptureStatusNone;
     }
     const bool capturing = cap == hipStreamCaptureStatusActive;
+    if (capturing && !e->allow_capture) {
+        // a captured step bakes this call's RNG step index (native re-init)
+        // or fresh candidates (reference RNG) into the graph: every replay
+        // would re-initialise finished envs with the same draws
+        PyErr_SetString(PyExc_RuntimeError,
+                        "Env.step under stream capture replays this step's re-init draws on "
+                        "every graph replay; set env.allow_graph_capture = True to accept "
+                        "that (timing runs)");
+        return nullptr;
+    }
     OutSet *s = take_set(e, capturing);
     if (!s) return nullptr;
     MarlnavStepBuffers b = e->base;
@@ -306,6 +317,7 @@ int Engine_init(Engine *e, PyObject *args, PyObject *)
     memset(&e->base, 0, sizeof(e->base));
     e->fast_ok = 0;
     e->write_norm = 0;
+    e->allow_capture = 0;
     e->step_idx = 1;
     e->steps_done = 0;
     e->next = 0;
@@ -442,6 +454,8 @@ PyMemberDef Engine_members[] = {
     {"step_idx", T_ULONGLONG, offsetof(Engine, step_idx), 0, "native RNG step counter"},
     {"steps_done", T_ULONGLONG, offsetof(Engine, steps_done), READONLY, "launched steps"},
     {"fast_ok", T_INT, offsetof(Engine, fast_ok), 0, "fast path enabled"},
+    {"allow_capture", T_INT, offsetof(Engine, allow_capture), 0,
+     "accept launches under stream capture"},
     {nullptr, 0, 0, 0, nullptr}};
 
 PyTypeObject EngineType = {PyVarObject_HEAD_INIT(nullptr, 0)};

@@ -212,6 +212,20 @@ class Env(object):
         self._configure()
 
     # ------------------------------------------------------------ plumbing
+    @property
+    def allow_graph_capture(self):
+        """Whether Env.step may be captured into a hipGraph (torch.cuda.graph).
+        A captured step fixes the re-init draws of that call (the native RNG's
+        step index, or the reference sampler's candidates), so every replay
+        re-initialises finished envs identically: accepted only when set
+        (timing runs such as bench.py's kernel_time_us); off by default, when
+        a captured step raises."""
+        return bool(self.__dict__['_engine'].allow_capture)
+
+    @allow_graph_capture.setter
+    def allow_graph_capture(self, on):
+        self.__dict__['_engine'].allow_capture = 1 if on else 0
+
     def __setattr__(self, name, value):
         if name in _PARAM_ATTRS or name == '_init_sampler':
             object.__setattr__(self, '_params_dirty', True)

@@ -1,6 +1,7 @@
 """Parity of the HIP step (libmarlnav.so through the drop-in Env) with the
 reference's golden vectors and with the C oracle. Needs an MI355X."""
 import os
+import warnings
 
 import numpy as np
 import pytest
@@ -954,3 +955,34 @@ def test_mappo_get_data_rollout_matches_reference(pkg):
     assert abs(float(mean) - float(z["mean_rew"])) <= 1e-5 * abs(float(z["mean_rew"]))
     assert (env._num_trunc, env._num_col, env._num_tar) == (m["num_trunc"], m["num_col"],
                                                             m["num_tar"])
+
+
+def test_graph_capture_needs_explicit_opt_in(pkg):
+    """A captured Env.step bakes its re-init draws into the graph:
+    capture raises unless env.allow_graph_capture is set; with it, replays
+    run the captured step (bench.py's kernel_time_us)."""
+    env = make_env(pkg, 1024, 3, 3, episode_len=200, seed=3)
+    acts = torch.zeros(1024, 3, 2, device=DEV)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        env.step(acts)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert not env.allow_graph_capture
+    g = torch.cuda.CUDAGraph()
+    with warnings.catch_warnings():  # torch notes the aborted capture is empty
+        warnings.simplefilter("ignore", UserWarning)
+        with pytest.raises(RuntimeError, match="allow_graph_capture"):
+            with torch.cuda.graph(g):
+                env.step(acts)
+    torch.cuda.synchronize()
+    env.allow_graph_capture = True
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = env.step(acts)
+    before = np_(env.states).copy()
+    g.replay()
+    torch.cuda.synchronize()
+    assert not np.array_equal(np_(env.states), before)   # the replay stepped the env
+    assert out[1].shape == (1024,)
