@@ -1,5 +1,5 @@
 """Fixed overhead of bench.py's timed region (host clock minus GPU event
-region) for 20-step loops under three synchronisation variants; optional
+region) for 20-step loops under several synchronisation variants; optional
 hipDeviceScheduleSpin (argv[1] == 'spin', set before torch touches the GPU)."""
 import ctypes, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -21,7 +21,7 @@ e0.record(); e1.record(); e1.synchronize()
 for i in range(5):
     env.step(acts[i % len(acts)])
 torch.cuda.synchronize()
-for variant in ("device_sync", "event_then_device", "idle_sync_cost"):
+for variant in ("device_sync", "event_then_device", "query_spin_then_device", "idle_sync_cost"):
     res = []
     for rep in range(15):
         torch.cuda.synchronize()
@@ -35,6 +35,9 @@ for variant in ("device_sync", "event_then_device", "idle_sync_cost"):
         e1.record()
         if variant == "event_then_device":
             e1.synchronize()
+        if variant == "query_spin_then_device":
+            while not e1.query():
+                pass
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) * 1e6
         reg = e0.elapsed_time(e1) * 1e3
