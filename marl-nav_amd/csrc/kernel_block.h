@@ -93,10 +93,10 @@ __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float
 }
 
 
-// Phases (one block barrier after each): stage | move + coordinate check
-// (moved states start streaming out) | observe into LDS rows | rows stream
-// out while wave 0 runs the per-env phase | re-init, re-observe and re-store
-// the finished envs only (none in most blocks).
+// Phases (one block barrier after each of the first four): stage | move +
+// coordinate check | observe into LDS rows | per-env phase on wave 0 while
+// waves 1..A-1 re-initialise and re-observe the finished envs (native
+// re-init; none in most blocks) | rows and states stream out of LDS.
 template <int A, int O, bool OBS_ONLY, bool NOISY>
 __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
 {

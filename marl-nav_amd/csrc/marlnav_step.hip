@@ -26,9 +26,10 @@
 // Numerics: built with -ffp-contract=off and the HIP default
 // correctly rounded fp32 division and sqrt, so every distance, dot product
 // and reward term is the fp32 expression the reference's CPU path evaluates,
-// summed in torch's order. sin/cos of the heading update are evaluated in
-// double (sincos_k, identical code in oracle/marlnav_oracle.c) and rounded
-// once; acos is the device libm's acosf.
+// summed in torch's order. sin/cos of the heading update are fp32 (<= 1 ulp:
+// Cody-Waite reduction and the Cephes polynomials, sincos_k, the same
+// operation sequence as oracle_sincos in oracle/marlnav_oracle.c); acos is
+// the device libm's acosf.
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
