@@ -70,6 +70,15 @@ struct SplitFinList {
     }
 };
 
+// The workgroup's finished envs as one list built by wave 0's per-env
+// phase (workgroup-spread shapes): env codes wave * EPW + env.
+struct FlatFinList {
+    const int *slot;
+    int n;
+    __device__ int total() const { return n; }
+    __device__ int operator[](int fe) const { return slot[fe]; }
+};
+
 // Finished envs re-initialised and re-observed by the whole workgroup
 // (after one block barrier) instead of by their own wave: pays where an
 // env's re-observation is long (measured: A3/O8 and A16/O32 faster, A3/O3
@@ -106,7 +115,10 @@ struct SplitPlan {
     // after the waves' regions: finished-env counts and slots of the
     // workgroup, the `unclean` word (reinit_block), then (kSplitTpl) the
     // formation and template at FTP
-    static constexpr int FTP = (kWavesPerBlock * (1 + EPW) + 1 + 3) & ~3;
+    // (+ kWavesPerBlock * EPW step numbers and as many `terminates` flags:
+    // the workgroup's per-env inputs, parked for wave 0's per-env phase)
+    static constexpr int ENVIN = (kWavesPerBlock * (1 + EPW) + 1 + 3) & ~3;
+    static constexpr int FTP = (ENVIN + 2 * kWavesPerBlock * EPW + 3) & ~3;
     static constexpr int BLK = FTP + (kSplitTpl<A, O> ? NCP : 0);
     static_assert(EPW >= 1, "an env's rows must fit one wave");
 };
@@ -445,11 +457,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
 
     if (!OBS_ONLY) {
         wave_sync();
-        // ---- per-env reductions, terminal logic, masked re-init
-        bool fin = false, tr_l = false, co_l = false, ta_l = false;
-        if (env_on) {
-            const int64_t e = e0 + lane;
-            const float4 *red = reinterpret_cast<const float4 *>(wl + SP::RED) + A * lane;
+        // ---- per-env reductions, terminal logic, masked re-init (env e,
+        // reward rows `red` (A float4: r_miss, r_hit, flags), step number and
+        // `terminates` in); returns fin and sets the counter flags
+        bool tr_l = false, co_l = false, ta_l = false;
+        const auto per_env = [&](int64_t e, const float4 *red, float sn_v, unsigned term_v,
+                                 float *s5, float *obl, float *tgl) -> bool {
             unsigned any_col = 0u, all_in = 1u;
             float rm[A], rh[A];
 #pragma unroll
@@ -466,14 +479,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
             for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
             const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
             out_st(&b.reward[e], rsum / (float)A);             // torch.mean (:233)
-            float step_num = sn_in + 1.0f;                     // :96
+            float step_num = sn_v + 1.0f;                      // :96
             const bool truncated = step_num > pr.trunc_after;  // :97
-            const bool term_old = term_in != 0u;
+            const bool term_old = term_v != 0u;
             const bool terminated = any_col || term_old;       // :213-214
             out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
             out_st(&b.terminated[e], (uint8_t)terminated);
             out_st(&b.truncated[e], (uint8_t)truncated);
-            fin = truncated || terminated;                     // :102-104
+            const bool fin = truncated || terminated;          // :102-104
             if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
                 KArgsK *kl = kargs_late();
                 MarlnavParams p;  // the fields the re-init reads
@@ -486,9 +499,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
                 p.angle_range = kl->p.angle_range;
                 p.flags = kl->p.flags;
                 p.seed = kl->p.seed;
-                float *s5 = st + 5 * A * lane;
-                float *obl = wl + SP::OB + 2 * O * lane;
-                float *tgl = wl + SP::TG + 2 * lane;
                 const float *fs = kl->a.b.fresh_states;
                 float *gob = kl->a.b.obstacles;
                 float *gtg = kl->a.b.target;
@@ -514,33 +524,55 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
             tr_l = truncated;
             co_l = any_col;
             ta_l = all_in;
-        }
-        const uint64_t finmask = __ballot(fin);
-        c_trunc = __popcll(__ballot(tr_l));
-        c_col = __popcll(__ballot(co_l));
-        c_tar = __popcll(__ballot(ta_l));
-        STAMP(4);
+            return fin;
+        };
 
         if constexpr (kSplitSpread<A, O>) {
             // ---- the workgroup's finished envs, re-initialised (:104) and
             // re-observed (:105) by all its threads: a finished env costs its
             // wave ~1/4 of a full observation pass instead of a second pass
-            // on its own lanes (the straggler that set the kernel's end)
+            // on its own lanes (the straggler that set the kernel's end).
+            // The per-env phase of all the workgroup's envs runs on wave 0
+            // (one lane per env) after one barrier, instead of on one or two
+            // lanes of every wave: the other waves' VALU is not spent on it.
             int *bcnt = reinterpret_cast<int *>(lds + kWavesPerBlock * SP::FLOATS);
             int *bslot = bcnt + kWavesPerBlock;
             int *unclean = bslot + kWavesPerBlock * EPW;
+            float *bsn = reinterpret_cast<float *>(bcnt) + SP::ENVIN;
+            unsigned *bterm = reinterpret_cast<unsigned *>(bsn + kWavesPerBlock * EPW);
             if (threadIdx.x == 0) *unclean = 0;
-            if (fin)
-                bslot[wib * EPW + (int)__builtin_amdgcn_mbcnt_hi(
-                                      (unsigned)(finmask >> 32),
-                                      __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] =
-                    wib * EPW + (int)lane;
-            if (lane == 0) bcnt[wib] = (int)__popcll(finmask);
-            __syncthreads();
+            if (env_on) {
+                bsn[wib * EPW + (int)lane] = sn_in;
+                bterm[wib * EPW + (int)lane] = term_in;
+            }
             const int64_t blk0 = (int64_t)blockIdx.x * kWavesPerBlock;
             const int live = (int)(K->a.ntiles - blk0 < kWavesPerBlock ? K->a.ntiles - blk0
                                                                       : kWavesPerBlock);
-            const SplitFinList<EPW> list = SplitFinList<EPW>::make(bcnt, bslot, live);
+            __syncthreads();
+            STAMP(4);
+            if (wib == 0) {
+                const int ce = (int)lane;  // env code: wave ce / EPW, env ce % EPW
+                const int64_t e = blk0 * EPW + ce;
+                const bool on = ce < live * EPW && e < P;
+                bool fin = false;
+                if (on) {
+                    const int cw = ce / EPW, cl = ce - cw * EPW;
+                    float *wlc = lds + cw * SP::FLOATS;
+                    fin = per_env(e, reinterpret_cast<const float4 *>(wlc + SP::RED) + A * cl,
+                                  bsn[ce], bterm[ce], wlc + SP::ST + 5 * A * cl,
+                                  wlc + SP::OB + 2 * O * cl, wlc + SP::TG + 2 * cl);
+                }
+                const uint64_t fm = __ballot(fin);
+                if (fin)
+                    bslot[__builtin_amdgcn_mbcnt_hi((unsigned)(fm >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] = ce;
+                if (lane == 0) bcnt[0] = (int)__popcll(fm);
+                c_trunc = __popcll(__ballot(tr_l));
+                c_col = __popcll(__ballot(co_l));
+                c_tar = __popcll(__ballot(ta_l));
+            }
+            __syncthreads();
+            const FlatFinList list{bslot, bcnt[0]};
 #if MARLNAV_STAMPS
             stamp_nfin = list.total();
 #endif
@@ -588,7 +620,18 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
                 }
                 __syncthreads();
             }
-        } else if (finmask) {
+        } else {
+            bool fin = false;
+            if (env_on)
+                fin = per_env(e0 + lane, reinterpret_cast<const float4 *>(wl + SP::RED) + A * lane,
+                              sn_in, term_in, st + 5 * A * lane, wl + SP::OB + 2 * O * lane,
+                              wl + SP::TG + 2 * lane);
+            const uint64_t finmask = __ballot(fin);
+            c_trunc = __popcll(__ballot(tr_l));
+            c_col = __popcll(__ballot(co_l));
+            c_tar = __popcll(__ballot(ta_l));
+            STAMP(4);
+            if (finmask) {
             // ---- observations of re-initialised envs (:105), on the wave
             wave_sync();
             const bool redo = row_on && ((finmask >> el) & 1u);
@@ -608,6 +651,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
                 else
                     split_pairs<A, O, LPR, false, false>(sts, obe, tge, a, q, rx, ry, rdx, rdy,
                                                         orow, brow, pr, unused);
+            }
             }
         }
     }
