@@ -374,6 +374,37 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
     }
     STAMP(2);
 
+    // per-agent reward of a row (environment.py:184-234) from its reduced
+    // terms: target bearing/distance, flags (1 ob_risk, 2 ob_col, 4 ag_risk,
+    // 8 ag_col), in-band count and its A-1 bond terms (LDS):
+    // (r_miss, r_hit, flags: 1 collision, 2 in target, 0)
+    const auto row_reward = [&](float ta, float td, unsigned fl, int band,
+                                const float *bond_row) -> float4 {
+        const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+        const float bandf = (float)band;
+        const float bandc = bandf < pr.max_at_prop_d ? bandf : pr.max_at_prop_d;
+        float bv[A - 1];
+#pragma unroll
+        for (int i = 0; i < A - 1; ++i) bv[i] = bond_row[i];
+        const float bond = torch_row_sum_r<A - 1>(bv, [](float x) { return x; });
+        const float dsc = bandc / pr.max_at_prop_d;
+        const float soft = -1.0f * (td / pr.init_dist);
+        const float bondm = bond / (float)(A - 1);
+        const float risk = (fl & 5u) ? 1.0f : 0.0f;
+        float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
+        float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
+        rm = rm + pr.distance_factor * dsc;
+        rh = rh + pr.distance_factor * dsc;
+        rm = rm + pr.soft_factor * soft;
+        rh = rh + pr.soft_factor * soft;
+        rm = rm + pr.bond_factor * bondm;
+        rh = rh + pr.bond_factor * bondm;
+        rm = rm - pr.risk_factor * risk;
+        rh = rh - pr.risk_factor * risk;
+        const unsigned flags = ((fl & 10u) ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u);
+        return make_float4(rm, rh, __uint_as_float(flags), 0.0f);
+    };
+
     // ---- observations + per-lane reward terms (:99-100)
     const float *sts = st + 5 * A * el;
     const float *obe = wl + SP::OB + 2 * O * el;
@@ -406,30 +437,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
                     t.ta = orow[0];  // computed by lane LPR-1 (wave_sync above)
                     t.td = orow[1];
                 }
-                const float head = fabsf(t.ta) < pr.max_angle_diff ? 1.0f : 0.0f;
-                const float bandf = (float)band;
-                const float bandc = bandf < pr.max_at_prop_d ? bandf : pr.max_at_prop_d;
-                float bv[A - 1];
-#pragma unroll
-                for (int i = 0; i < A - 1; ++i) bv[i] = brow[i];
-                const float bond = torch_row_sum_r<A - 1>(bv, [](float x) { return x; });
-                const float dsc = bandc / pr.max_at_prop_d;
-                const float soft = -1.0f * (t.td / pr.init_dist);
-                const float bondm = bond / (float)(A - 1);
-                const float risk = (fl & 5u) ? 1.0f : 0.0f;
-                float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
-                float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
-                rm = rm + pr.distance_factor * dsc;
-                rh = rh + pr.distance_factor * dsc;
-                rm = rm + pr.soft_factor * soft;
-                rh = rh + pr.soft_factor * soft;
-                rm = rm + pr.bond_factor * bondm;
-                rh = rh + pr.bond_factor * bondm;
-                rm = rm - pr.risk_factor * risk;
-                rh = rh - pr.risk_factor * risk;
-                const unsigned flags = ((fl & 10u) ? 1u : 0u) | ((t.td < pr.target_radius) ? 2u : 0u);
-                reinterpret_cast<float4 *>(wl + SP::RED)[row] =
-                    make_float4(rm, rh, __uint_as_float(flags), 0.0f);
+                if constexpr (kSplitSpread<A, O>) {
+                    // the row's reduced terms; wave 0 finishes every row of
+                    // the workgroup after the barrier (row_reward)
+                    reinterpret_cast<float4 *>(wl + SP::RED)[row] =
+                        make_float4(t.ta, t.td, __uint_as_float(fl), __int_as_float(band));
+                } else {
+                    reinterpret_cast<float4 *>(wl + SP::RED)[row] =
+                        row_reward(t.ta, t.td, fl, band, brow);
+                }
             }
         }
     }
@@ -551,6 +567,19 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
             __syncthreads();
             STAMP(4);
             if (wib == 0) {
+                // every row of the workgroup: its reward terms (one lane per
+                // row, all 64 lanes busy where the row leaders were 1 in LPR)
+                static_assert(kWavesPerBlock * R <= 64, "one lane per row of the workgroup");
+                if ((int)lane < live * R) {
+                    const int cw = (int)lane / R, rw = (int)lane - cw * R;
+                    float *wlc = lds + cw * SP::FLOATS;
+                    float4 *rp = reinterpret_cast<float4 *>(wlc + SP::RED) + rw;
+                    const float4 tv = *rp;
+                    if ((blk0 + cw) * EPW + rw / A < P)
+                        *rp = row_reward(tv.x, tv.y, __float_as_uint(tv.z), __float_as_int(tv.w),
+                                         wlc + SP::BOND + rw * (A - 1));
+                }
+                wave_sync();
                 const int ce = (int)lane;  // env code: wave ce / EPW, env ce % EPW
                 const int64_t e = blk0 * EPW + ce;
                 const bool on = ce < live * EPW && e < P;
