@@ -206,6 +206,9 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     constexpr int TQ = LPR - 1;  // the lane whose last other-agent / obstacle slot is spare
     const float cap = pr.cap_distance;
     SplitTerms t{0u, 0, 0.0f, 0.0f};
+    // obstacle flags from the nearest obstacle (d < r for some d <=> min d <
+    // r; v_min ignores a NaN distance, which compares false either way)
+    float ob_min = __builtin_inff();
     if constexpr (!kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>) {
         const float d = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
         const float ang = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, d, cap, ok);
@@ -231,8 +234,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
             if (valid) {
                 orow[2 + j] = ang;
                 orow[2 + O + j] = d;
-                if (TERMS)
-                    t.fl |= (d < pr.ob_risk_dist ? 1u : 0u) | (d < pr.ob_coll_dist ? 2u : 0u);
+                if (TERMS) ob_min = __builtin_fminf(ob_min, d);
             } else {
                 orow[0] = ang;
                 orow[1] = d;
@@ -267,6 +269,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
             }
         }
     }
+    if (TERMS) t.fl |= (ob_min < pr.ob_risk_dist ? 1u : 0u) | (ob_min < pr.ob_coll_dist ? 2u : 0u);
     return t;
 }
 
