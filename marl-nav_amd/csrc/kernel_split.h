@@ -193,7 +193,7 @@ constexpr bool kSplitTgtInOb = !kSplitTgtInAg<A, O, LPR> && O % LPR != 0;
 
 // unroll factor of split_pairs' obstacle / other-agent loops (timing builds)
 
-template <int A, int O, int LPR, bool TERMS, bool FAST>
+template <int A, int O, int LPR, bool TERMS, bool FAST, bool TFAST = false>
 __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
                                                   const float *__restrict__ obe,
                                                   const float *__restrict__ tge, int a, int q,
@@ -209,6 +209,11 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     // obstacle flags from the nearest obstacle (d < r for some d <=> min d <
     // r; v_min ignores a NaN distance, which compares false either way)
     float ob_min = __builtin_inff();
+    // TFAST (FAST tiles, parameters inside the short sequences' guards,
+    // kTermsFastFlag): the bond terms' divisions by the exact short sequences
+    static_assert(!TFAST || FAST, "short divisions need the fast coordinate range");
+    DivC d_sharp{1.0f, 1.0f};
+    if constexpr (TERMS && TFAST) d_sharp = make_divc(pr.bond_sharpness, ok);
     if constexpr (!kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>) {
         const float d = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
         const float ang = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, d, cap, ok);
@@ -263,8 +268,13 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
                 if (TERMS) {
                     t.fl |= (d < pr.ag_risk_dist ? 4u : 0u) | (d < pr.ag_coll_dist ? 8u : 0u);
                     t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
-                    const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
-                    bond_row[kx] = 1.0f / (1.0f + sd * sd);
+                    if constexpr (TFAST) {
+                        const float sd = div_c(d - pr.ideal_dist, d_sharp, ok);
+                        bond_row[kx] = recip_fast(1.0f + sd * sd, ok);
+                    } else {
+                        const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
+                        bond_row[kx] = 1.0f / (1.0f + sd * sd);
+                    }
                 }
             }
         }
@@ -425,7 +435,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
         }
         bool unused = true;
         SplitTerms t;
-        if (__builtin_expect(fast, 1))
+        if (__builtin_expect(fast, 1) && !OBS_ONLY && (pr.flags & kTermsFastFlag))
+            t = split_pairs<A, O, LPR, !OBS_ONLY, true, true>(sts, obe, tge, a, q, ox, oy, dx, dy,
+                                                             orow, brow, pr, unused);
+        else if (__builtin_expect(fast, 1))
             t = split_pairs<A, O, LPR, !OBS_ONLY, true>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
                                                        brow, pr, unused);
         else

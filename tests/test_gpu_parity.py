@@ -622,8 +622,8 @@ def test_reward_term_divisions_bit_exact_for_any_parameters(pkg, geom, shape):
     kernels use the short exact division sequences only when the host finds
     every such parameter inside their guards (marlnav_step, terms_fast_params)
     and IEEE division otherwise (the block kernel; the split kernel, the
-    second shape, always divides with IEEE division). Rewards stay bit-exact
-    vs the oracle (which divides with IEEE division) either way."""
+    second shape, for its bond terms). Rewards stay bit-exact vs the oracle
+    (which divides with IEEE division) either way."""
     P, A, O = shape
     g = torch.Generator().manual_seed(77)
     env = make_env(pkg, P, A, O, episode_len=40, seed=3,
