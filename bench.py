@@ -23,8 +23,10 @@ back-to-back Env.step launches (of a second Env of the same shape, so the
 timed env's state and counters are untouched); ``achieved`` = algorithmic
 bytes per launch (read 28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at
 A3/O3) / ``kernel_us``, against the 8 TB/s HBM peak. ``timed_region_us`` =
-HIP events on the same stream around the K timed steps, per step (includes
-any gap the host leaves between launches). ``traffic``: HBM bytes per launch
+HIP events on the launch stream around a second, untimed pass of the same K
+steps, per step (includes any gap the host leaves between launches); the
+timed pass itself carries no events (recording one there adds ~13 us of
+GPU-side marker processing per region, scripts/diag/sync_overhead.py). ``traffic``: HBM bytes per launch
 from the committed rocprofv3 PMC summary for this config (profiles/; not
 measured in this run - the source is named), or null.
 
@@ -267,19 +269,32 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    # the timed region: exactly K steps between barrier + synchronize pairs,
+    # with no instrumentation inside (a timing-event record in the region
+    # costs ~13 us of GPU marker processing per region at 65536 envs:
+    # scripts/diag/sync_overhead.py, profiles/r02_sync_overhead.txt)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev0.record()
     for i in range(a.steps):
         env.step(actions[i % len(actions)])
-    ev1.record()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
     dt = pkg.shard.max_over_ranks(dt, red_dev)
-    region_us = ev0.elapsed_time(ev1) * 1e3 / a.steps
     counters = pkg.shard.sum_over_ranks([env._num_trunc, env._num_col, env._num_tar], red_dev)
+
+    # the same K steps again with HIP events on the launch stream around
+    # them: the GPU-side time per step of the timed loop (diagnostic; not
+    # the value)
+    barrier()
+    torch.cuda.synchronize()
+    ev0.record()
+    for i in range(a.steps):
+        env.step(actions[(a.steps + i) % len(actions)])
+    ev1.record()
+    torch.cuda.synchronize()
+    region_us = ev0.elapsed_time(ev1) * 1e3 / a.steps
 
     kenv = make_env(pkg, P, A, O, device, rank, seed=20251004)
     kern_us, kern_med = kernel_time_us(kenv, actions)

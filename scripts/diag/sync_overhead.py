@@ -1,5 +1,6 @@
 """Fixed overhead of bench.py's timed region (host clock minus GPU event
-region) for 20-step loops under several synchronisation variants; optional
+region) for 20-step loops: events recorded inside the region (bench.py), ev0
+recorded before t0, no events; optional
 hipDeviceScheduleSpin (argv[1] == 'spin', set before torch touches the GPU)."""
 import ctypes, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -21,26 +22,27 @@ e0.record(); e1.record(); e1.synchronize()
 for i in range(5):
     env.step(acts[i % len(acts)])
 torch.cuda.synchronize()
-for variant in ("device_sync", "event_then_device", "query_spin_then_device", "idle_sync_cost"):
+KUS = bench.kernel_time_us(bench.make_env(pkg, P, A, O, dev, 0, seed=7), acts)[1]
+print(f"graph-replay kernel time {KUS:.2f} us; overhead = host time of 20 steps - 20 x that")
+for variant in ("device_sync", "ev0_before_t0", "no_events", "idle_sync_cost"):
     res = []
     for rep in range(15):
         torch.cuda.synchronize()
         if variant == "idle_sync_cost":
             t0 = time.perf_counter(); torch.cuda.synchronize(); res.append((time.perf_counter() - t0) * 1e6)
             continue
+        if variant == "ev0_before_t0":
+            e0.record()
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
-        e0.record()
+        if variant == "device_sync":
+            e0.record()
         for i in range(20):
             env.step(acts[i % len(acts)])
-        e1.record()
-        if variant == "event_then_device":
-            e1.synchronize()
-        if variant == "query_spin_then_device":
-            while not e1.query():
-                pass
+        if variant != "no_events":
+            e1.record()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) * 1e6
-        reg = e0.elapsed_time(e1) * 1e3
-        res.append(dt - reg)
+        res.append(dt - 20 * KUS)
     res.sort()
     print(f"{variant}: overhead us median {res[len(res)//2]:.1f} min {res[0]:.1f} max {res[-1]:.1f}", flush=True)
