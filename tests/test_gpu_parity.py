@@ -989,3 +989,51 @@ def test_graph_capture_needs_explicit_opt_in(pkg):
     torch.cuda.synchronize()
     assert not np.array_equal(np_(env.states), before)   # the replay stepped the env
     assert out[1].shape == (1024,)
+
+
+@pytest.mark.parametrize("P,A,O", [(4096, 3, 3), (4096 + 37, 3, 3), (2048 + 5, 3, 8)])
+def test_collisions_at_the_threshold_ulp_bit_exact_vs_oracle(pkg, P, A, O):
+    """Collision tests d < c (environment.py:207-214) on distances from the
+    env-block kernel's short correctly rounded sqrt, at the threshold's ulp:
+    agent-obstacle distances within +-8 ulps of ob_coll_dist and agent-agent
+    distances within +-8 ulps of ag_coll_dist, one offset per env (full and
+    ragged last blocks, O3 and O8): terminated flags, re-initialised states
+    and the re-observed rows equal the oracle's bit for bit."""
+    env = make_env(pkg, P, A, O, episode_len=50, seed=21)
+    e = np.arange(P)
+    k = (e % 17) - 8                         # ulp offset of this env
+    st = np.zeros((P, A, 5), np.float32)
+    st[:, :, 0] = -3.0                        # heading +x, speed 3, turn 0, accel 0:
+    st[:, :, 2] = 1.0                         # every agent moves exactly to x = 0
+    st[:, :, 4] = 3.0
+    st[:, 0, 1] = 0.0
+    st[:, 1, 1] = 1000.0
+    st[:, 2, 1] = 2000.0
+    pair = e % 3 == 1                         # every third env: agents 0, 1 at ~5
+    y1 = np.float32(5.0) + k.astype(np.float32) * np.float32(2.0 ** -21)
+    st[pair, 1, 1] = y1[pair]
+    ob = np.full((P, O, 2), 4000.0, np.float32)
+    ob[:, :, 1] += np.arange(O, dtype=np.float32) * 100.0
+    near = e % 3 != 1                         # the others: obstacle 0 at ~50 from agent 0
+    ob[near, 0, 0] = (np.float32(50.0) + k.astype(np.float32) * np.float32(2.0 ** -18))[near]
+    ob[near, 0, 1] = 0.0
+    tg = np.full((P, 1, 2), -5000.0, np.float32)
+    env.states = torch.from_numpy(st)
+    env.obstacles = torch.from_numpy(ob)
+    env.target = torch.from_numpy(tg)
+    dm, pr = oracle_params(env)
+    form = np_(env._formation)
+    acts = [np.zeros((P, A, 2), np.float32) for _ in range(2)]
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    exp1 = orc.step(dm, pr, st, ob, tg, sn, te, acts[0], formation=form, step_idx=1)
+    n_col = int(exp1["terminated"].sum())
+    assert 0.3 * P < n_col < 0.7 * P, n_col   # both sides of the threshold are hit
+    lib = env._lib
+    prev = lib.marlnav_debug_force_family(1)  # MARLNAV_FAMILY_BLOCK
+    try:
+        _run_vs_oracle(env, dm, pr, st, ob, tg, sn, te, acts, form=form,
+                       where=f"P{P} A{A} O{O}")
+        assert lib.marlnav_debug_last_family() == 1
+    finally:
+        lib.marlnav_debug_force_family(prev)
