@@ -18,7 +18,14 @@ __global__ void probe(uint32_t base, unsigned long long *cnt, unsigned long long
     if (__float_as_uint(a) != __float_as_uint(b)) {
         const unsigned long long k = atomicAdd(cnt, 1ull);
         if (k < 8) ex[k] = u;
-        if (x >= 0x1p-96f && x <= 0x1p96f) atomicAdd(cnt_fast, 1ull);
+        if (x >= 0x1p-96f && x <= 0x1p96f) {
+            atomicAdd(cnt_fast, 1ull);
+            // direction inside the FAST range: v_sqrt above / below the
+            // correctly rounded value, and by more than one ulp
+            const int d = (int)__float_as_uint(a) - (int)__float_as_uint(b);
+            atomicAdd(cnt_fast + (d > 0 ? 1 : 2), 1ull);
+            if (d > 1 || d < -1) atomicAdd(cnt_fast + 3, 1ull);
+        }
     }
 }
 
@@ -27,10 +34,10 @@ int main()
     unsigned long long *cnt, *cf;
     uint32_t *ex;
     hipMalloc(&cnt, 8);
-    hipMalloc(&cf, 8);
+    hipMalloc(&cf, 32);
     hipMalloc(&ex, 32);
     hipMemset(cnt, 0, 8);
-    hipMemset(cf, 0, 8);
+    hipMemset(cf, 0, 32);
     hipMemset(ex, 0, 32);
     const uint32_t chunk = 1u << 28;
     for (uint64_t b = 0; b <= 0x7f7fffffull; b += chunk)
@@ -40,7 +47,10 @@ int main()
     hipMemcpy(&h, cnt, 8, hipMemcpyDeviceToHost);
     hipMemcpy(&hf, cf, 8, hipMemcpyDeviceToHost);
     hipMemcpy(he, ex, 32, hipMemcpyDeviceToHost);
-    printf("v_sqrt_f32 != IEEE sqrtf: %llu of 2139095040 positive finite floats; %llu inside [2^-96, 2^96]\n", h, hf);
+    unsigned long long hd[4];
+    hipMemcpy(hd, cf, 32, hipMemcpyDeviceToHost);
+    printf("v_sqrt_f32 != IEEE sqrtf: %llu of 2139095040 positive finite floats; %llu inside [2^-96, 2^96]"
+           " (v_sqrt above: %llu, below: %llu, off by more than 1 ulp: %llu)\n", h, hf, hd[1], hd[2], hd[3]);
     for (int i = 0; i < 8 && i < (int)h; ++i) printf("  x bits 0x%08x (%g)\n", he[i], (double)__builtin_bit_cast(float, he[i]));
     return 0;
 }
