@@ -2,10 +2,24 @@
 // correctly rounded sqrtf (hipcc's sequence: v_sqrt + residual fix-up) over
 // every positive finite float, and inside the FAST range [2^-96, 2^96] that
 // sqrt_fast (device_math.h) guards. Prints mismatch counts and examples.
-// Build: hipcc --offload-arch=gfx950 -O3 sqrt_probe.hip -o sqrt_probe
-#include <hip/hip_runtime.h>
-#include <stdio.h>
-#include <stdint.h>
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 sqrt_probe.hip -o sqrt_probe
+// Also: the shipped sqrt_fast (marl-nav_amd/csrc/device_math.h) against
+// IEEE sqrtf over every float of its range [2^-96, 2^96] and zero.
+#include "../../marl-nav_amd/csrc/marlnav_step.hip"
+
+__global__ void probe_fast(uint32_t base, unsigned long long *cnt, uint32_t *ex)
+{
+    const uint32_t u = base + blockIdx.x * blockDim.x + threadIdx.x;
+    const float x = __uint_as_float(u);
+    if (!((x >= 0x1p-96f && x <= 0x1p96f) || u == 0u)) return;
+    bool ok = true;
+    const float a = sqrt_fast(x, ok);
+    const float b = __builtin_sqrtf(x);
+    if (__float_as_uint(a) != __float_as_uint(b) || !ok) {
+        const unsigned long long k = atomicAdd(cnt, 1ull);
+        if (k < 8) ex[k] = u;
+    }
+}
 
 __global__ void probe(uint32_t base, unsigned long long *cnt, unsigned long long *cnt_fast,
                       uint32_t *ex)
@@ -52,5 +66,19 @@ int main()
     printf("v_sqrt_f32 != IEEE sqrtf: %llu of 2139095040 positive finite floats; %llu inside [2^-96, 2^96]"
            " (v_sqrt above: %llu, below: %llu, off by more than 1 ulp: %llu)\n", h, hf, hd[1], hd[2], hd[3]);
     for (int i = 0; i < 8 && i < (int)h; ++i) printf("  x bits 0x%08x (%g)\n", he[i], (double)__builtin_bit_cast(float, he[i]));
-    return 0;
+    unsigned long long *cq;
+    uint32_t *eq;
+    hipMalloc(&cq, 8);
+    hipMalloc(&eq, 32);
+    hipMemset(cq, 0, 8);
+    for (uint64_t b = 0; b <= 0x7f7fffffull; b += chunk)
+        hipLaunchKernelGGL(probe_fast, dim3(chunk / 256), dim3(256), 0, 0, (uint32_t)b, cq, eq);
+    unsigned long long hq = 0;
+    uint32_t heq[8];
+    hipMemcpy(&hq, cq, 8, hipMemcpyDeviceToHost);
+    hipMemcpy(heq, eq, 32, hipMemcpyDeviceToHost);
+    printf("sqrt_fast != IEEE sqrtf: %llu floats of [2^-96, 2^96] and +0\n", hq);
+    for (int i = 0; i < 8 && i < (int)hq; ++i) printf("  x bits 0x%08x\n", heq[i]);
+    printf("hip: %s\n", hipGetErrorString(hipDeviceSynchronize()));
+    return hq == 0 ? 0 : 1;
 }
