@@ -22,13 +22,25 @@ struct KArgs {
 };
 typedef __attribute__((address_space(4))) const KArgs KArgsK;
 
-// Kernarg pointer the compiler cannot hoist loads through.
+// Kernarg pointer the compiler cannot hoist loads through. OFF: byte offset
+// of the KArgs argument in the kernarg segment (the env-block and pair-split
+// kernels pass their staging pointers first, kHotKargsOff).
+template <int OFF>
 __device__ __forceinline__ KArgsK *kargs_late()
 {
-    KArgsK *k = (KArgsK *)__builtin_amdgcn_kernarg_segment_ptr();
+    const char *p = (const char *)__builtin_amdgcn_kernarg_segment_ptr() + OFF;
+    KArgsK *k = (KArgsK *)p;
     asm volatile("" : "+s"(k));
     return k;
 }
+
+// The env-block and pair-split kernels' leading kernel arguments: the
+// pointers their staging reads and the env count, 14 dwords that the
+// dispatcher preloads into user SGPRs (Makefile:
+// -amdgpu-kernarg-preload-count=14), so a wave's first LDS-DMA does not wait
+// for a scalar load of the kernarg segment (65536x3x3 8.72 -> 8.47 us
+// median, A/B on one box). KArgs follows at kHotKargsOff.
+constexpr int kHotKargsOff = 7 * 8;
 
 template <class T>
 __device__ __forceinline__ T in_sgpr(T p)

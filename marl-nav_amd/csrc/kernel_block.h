@@ -98,11 +98,14 @@ __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
 // re-init; none in most blocks) | rows and states stream out of LDS.
 template <int A, int O, bool OBS_ONLY, bool NOISY>
-__global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
+__global__ void __launch_bounds__(64 * A)
+    block_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
+                 const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
+                 int64_t h_P, KArgs k)
 {
     using BP = BlockPlan<A, O>;
     constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
-    (void)k;  // read through kargs_late()
+    (void)k;  // read through kargs_late<kHotKargsOff>()
     extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS
     unsigned long long t_entry;
@@ -113,11 +116,17 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // agent of this wave
     const int64_t blk = blockIdx.x;
     const int64_t gw = blk * A + w;  // stamps slot
-    KArgsK *K = kargs_late();
-    const int64_t P = K->a.P;
-    // launch_block's grid is exactly ntiles blocks: no exit test, so the
-    // pointer loads below go out in the same round of kernarg loads as P
-    const StepPtrs b = load_ptrs(K);
+    KArgsK *K = kargs_late<kHotKargsOff>();
+    const int64_t P = h_P;
+    // launch_block's grid is exactly ntiles blocks: no exit test. The staging
+    // pointers come preloaded in SGPRs; the rest are read from KArgs.
+    StepPtrs b = load_ptrs(K);
+    b.states = h_states;
+    b.actions = h_actions;
+    b.obstacles = const_cast<float *>(h_obstacles);
+    b.target = const_cast<float *>(h_target);
+    b.step_num = const_cast<float *>(h_step_num);
+    b.terminates = const_cast<uint8_t *>(h_terminates);
     STAMP(0);
     float *st = lds + BP::ST;
     const int64_t e0 = blk * E;
@@ -186,7 +195,7 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
         const float2 act = reinterpret_cast<const float2 *>(lds + BP::ACT)[r];
         float a0 = act.x, a1 = act.y;
         if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
-            KArgsK *kl = kargs_late();
+            KArgsK *kl = kargs_late<kHotKargsOff>();
             a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
             a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
         }
@@ -255,7 +264,7 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
         const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
         // native (non-noisy) re-init: waves 1..A-1 take the finished envs
         // while wave 0 runs the per-env phase (below)
-        const bool overlap = !NOISY && !kargs_late()->a.b.fresh_states;
+        const bool overlap = !NOISY && !kargs_late<kHotKargsOff>()->a.b.fresh_states;
         // ---- per-env reductions, terminal logic (wave 0, one lane per env)
         if (w == 0) {
             const bool env_on = l < ne;
@@ -287,7 +296,7 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
                 out_st(&b.truncated[e], (uint8_t)truncated);
                 fin = truncated || terminated;                     // :102-104
                 if (NOISY && fin) {  // noisy native re-init: serial per env
-                    KArgsK *kl = kargs_late();
+                    KArgsK *kl = kargs_late<kHotKargsOff>();
                     {
                         MarlnavParams p;  // the fields the re-init reads
                         p.obs_range_x = kl->p.obs_range_x;
@@ -325,7 +334,7 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
             if (lane == 0) {
                 flg[0] = (int)__popcll(finmask);
                 if (c_trunc | c_col | c_tar) {
-                    KArgsK *kl = kargs_late();
+                    KArgsK *kl = kargs_late<kHotKargsOff>();
                     uint64_t *cnt = kl->a.b.counters;
                     const int64_t slots = kl->a.waves;
                     if (cnt) {
@@ -357,7 +366,7 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
                     wlist[__builtin_amdgcn_mbcnt_hi(
                         (unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] = l;
                 wave_sync();  // every lane of this wave sees its list
-                reinit_reobs_native<A, O>(kargs_late(), ev, lds + BP::FORM, wlist,
+                reinit_reobs_native<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, wlist,
                                           (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
             }
         }
@@ -368,7 +377,7 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
             // ---- reference-RNG / noisy re-init (:104; noisy: done above by
             // wave 0) and observations of the re-initialised envs (:105)
             if (!NOISY) {
-                reinit_block<A, O>(kargs_late(), ev, lds + BP::FORM, list, nfin, tid, NT);
+                reinit_block<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, list, nfin, tid, NT);
                 __syncthreads();
             }
             reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, NT);
@@ -382,7 +391,7 @@ __global__ void __launch_bounds__(64 * A) block_kernel(KArgs k)
     } else if (!OBS_ONLY) {
         block_store(gobs, obs_rows, nrow * D, tid, NT);
         if (norm) {
-            KArgsK *kl = kargs_late();
+            KArgsK *kl = kargs_late<kHotKargsOff>();
             const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
             float *gn = kl->a.b.obs_norm + e0 * (A * D);
             for (int i = tid; i < nrow * D; i += NT) {

@@ -287,11 +287,14 @@ template <int A, int O, int LPR, bool OBS_ONLY, bool NOISY>
 // (min 4 waves per SIMD: keeps the max-ilp scheduler (Makefile) within the
 // 128 VGPRs of the 4-waves-per-SIMD grids; unbounded it takes 178 at A16/O32
 // and halves occupancy)
-__global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
+__global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
+    split_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
+                 const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
+                 int64_t h_P, KArgs k)
 {
     using SP = SplitPlan<A, O, LPR>;
     constexpr int EPW = SP::EPW, R = SP::R, D = SP::D;
-    (void)k;  // read through kargs_late()
+    (void)k;  // read through kargs_late<kHotKargsOff>()
     extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS
     int stamp_nfin = 0;
@@ -304,16 +307,17 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wib;
     const int64_t tile = gw;
-    KArgsK *K = kargs_late();
-    const int64_t P = K->a.P;
-    // pointers first, pinned in SGPRs before the exit test: one round of
-    // kernarg loads ahead of the first wait (the compiler would otherwise
-    // sink them below the branch, a second serial round)
-    const StepPtrs b = load_ptrs(K);
-    const int64_t ntiles = K->a.ntiles;
-    asm volatile("" ::"s"(b.states), "s"(b.obstacles), "s"(b.target), "s"(b.actions),
-                 "s"(b.obs), "s"(ntiles), "s"(P));
-    if (tile >= ntiles) return;
+    KArgsK *K = kargs_late<kHotKargsOff>();
+    const int64_t P = h_P;
+    if (tile * EPW >= P) return;  // (launch_split: ntiles = ceil(P / EPW) tiles)
+    // the staging pointers come preloaded in SGPRs; the rest from KArgs
+    StepPtrs b = load_ptrs(K);
+    b.states = h_states;
+    b.actions = h_actions;
+    b.obstacles = const_cast<float *>(h_obstacles);
+    b.target = const_cast<float *>(h_target);
+    b.step_num = const_cast<float *>(h_step_num);
+    b.terminates = const_cast<uint8_t *>(h_terminates);
     STAMP(0);
     float *wl = lds + wib * SP::FLOATS;
     float *st = wl + SP::ST;
@@ -360,7 +364,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
         const float2 act = reinterpret_cast<const float2 *>(wl + SP::ACT)[rowc];
         float a0 = act.x, a1 = act.y;
         if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
-            KArgsK *kl = kargs_late();
+            KArgsK *kl = kargs_late<kHotKargsOff>();
             a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
             a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
         }
@@ -475,7 +479,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
     float cp[KCP];
     bool tpl_on = false;
     if constexpr (kSplitTpl<A, O> && !NOISY && !OBS_ONLY) {
-        KArgsK *kl = kargs_late();
+        KArgsK *kl = kargs_late<kHotKargsOff>();
         const float *cfo = kl->a.b.formation, *ctp = kl->a.b.formation_obs;
         tpl_on = ctp && !kl->a.b.fresh_states;
         if (tpl_on) {
@@ -520,7 +524,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
             out_st(&b.truncated[e], (uint8_t)truncated);
             const bool fin = truncated || terminated;          // :102-104
             if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
-                KArgsK *kl = kargs_late();
+                KArgsK *kl = kargs_late<kHotKargsOff>();
                 MarlnavParams p;  // the fields the re-init reads
                 p.obs_range_x = kl->p.obs_range_x;
                 p.obs_mean_x = kl->p.obs_mean_x;
@@ -622,7 +626,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
             stamp_nfin = list.total();
 #endif
             if (const int nfin = list.total()) {
-                KArgsK *kl = kargs_late();
+                KArgsK *kl = kargs_late<kHotKargsOff>();
                 const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
                     lds, blk0 * EPW};
                 // waves past the last tile have exited: items go to the live ones
@@ -712,7 +716,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
         float *gnorm = nullptr;
         const float *mean = nullptr, *scale = nullptr;
         if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
-            KArgsK *kl = kargs_late();
+            KArgsK *kl = kargs_late<kHotKargsOff>();
             gnorm = kl->a.b.obs_norm + e0 * (A * D);
             mean = kl->a.b.norm_mean;
             scale = kl->a.b.norm_scale;
@@ -759,7 +763,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4) split_kernel(KArgs k)
     }
     STAMP(6);
     if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
-        KArgsK *kl = kargs_late();
+        KArgsK *kl = kargs_late<kHotKargsOff>();
         uint64_t *cnt = kl->a.b.counters;
         const int64_t slots = kl->a.waves;
         if (cnt) {

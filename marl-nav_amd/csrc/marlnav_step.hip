@@ -201,7 +201,10 @@ const KernelPair kVariants[] = {
 };
 
 // Step kernels that take their arguments through one KArgs block
-using TileFn = void (*)(KArgs);
+// the env-block and pair-split kernels: staging pointers and P first
+// (kHotKargsOff, kernel_args.h), then KArgs
+using BlockFn = void (*)(float *, const float *, const float *, const float *, const float *,
+                         const uint8_t *, int64_t, KArgs);
 
 bool aligned(const void *p, uintptr_t n) { return (reinterpret_cast<uintptr_t>(p) & (n - 1)) == 0; }
 
@@ -209,7 +212,7 @@ bool aligned(const void *p, uintptr_t n) { return (reinterpret_cast<uintptr_t>(p
 // for one lane per row to fill the chip
 struct SplitVariant {
     int A, O, epw;
-    TileFn step, obs, noisy;
+    BlockFn step, obs, noisy;
     size_t lds;
     bool always;  // also for large grids
     int lpr;
@@ -263,7 +266,7 @@ const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers 
     return v;
 }
 
-int launch_split(const SplitVariant &v, TileFn fn, const StepArgs &args, const MarlnavParams &pr,
+int launch_split(const SplitVariant &v, BlockFn fn, const StepArgs &args, const MarlnavParams &pr,
                  void *stream, const char *what)
 {
     KArgs ka;
@@ -272,7 +275,13 @@ int launch_split(const SplitVariant &v, TileFn fn, const StepArgs &args, const M
     ka.a.W = v.epw;
     ka.a.ntiles = (args.P + v.epw - 1) / v.epw;
     const int64_t blocks = (ka.a.ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    void *kargs[] = {&ka};
+    float *h_states = args.b.states;
+    const float *h_actions = args.b.actions, *h_obstacles = args.b.obstacles,
+                *h_target = args.b.target, *h_step_num = args.b.step_num;
+    const uint8_t *h_terminates = args.b.terminates;
+    int64_t h_P = args.P;
+    void *kargs[] = {&h_states, &h_actions, &h_obstacles, &h_target, &h_step_num, &h_terminates,
+                     &h_P, &ka};
     hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)blocks),
                                    dim3(64 * kWavesPerBlock), kargs, v.lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
@@ -284,7 +293,7 @@ int launch_split(const SplitVariant &v, TileFn fn, const StepArgs &args, const M
 // them off (A/B timing against the tile kernels)
 struct BlockVariant {
     int A, O;
-    TileFn step, obs, noisy;
+    BlockFn step, obs, noisy;
     size_t lds;
 };
 
@@ -315,7 +324,7 @@ const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers 
     return v;
 }
 
-int launch_block(const BlockVariant &v, TileFn fn, const StepArgs &args, const MarlnavParams &pr,
+int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const MarlnavParams &pr,
                  void *stream, const char *what)
 {
     KArgs ka;
@@ -323,7 +332,14 @@ int launch_block(const BlockVariant &v, TileFn fn, const StepArgs &args, const M
     ka.p = pr;
     ka.a.W = BlockPlan<3, 3>::E;
     ka.a.ntiles = (args.P + ka.a.W - 1) / ka.a.W;
-    void *kargs[] = {&ka};
+    // the leading arguments (kHotKargsOff, kernel_args.h): staging pointers, P
+    float *h_states = args.b.states;
+    const float *h_actions = args.b.actions, *h_obstacles = args.b.obstacles,
+                *h_target = args.b.target, *h_step_num = args.b.step_num;
+    const uint8_t *h_terminates = args.b.terminates;
+    int64_t h_P = args.P;
+    void *kargs[] = {&h_states, &h_actions, &h_obstacles, &h_target, &h_step_num, &h_terminates,
+                     &h_P, &ka};
     hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)ka.a.ntiles),
                                    dim3(64 * v.A), kargs, v.lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
