@@ -1,6 +1,7 @@
 """Parity of the HIP step (libmarlnav.so through the drop-in Env) with the
 reference's golden vectors and with the C oracle. Needs an MI355X."""
 import os
+import subprocess
 import warnings
 
 import numpy as np
@@ -1037,3 +1038,53 @@ def test_collisions_at_the_threshold_ulp_bit_exact_vs_oracle(pkg, P, A, O):
         assert lib.marlnav_debug_last_family() == 1
     finally:
         lib.marlnav_debug_force_family(prev)
+
+
+@pytest.mark.parametrize("P,A,O,steps", [(20000 + 3, 3, 3, 12), (512, 16, 32, 6)])
+def test_c_host_matches_python_env(pkg, P, A, O, steps, tmp_path):
+    """The C ABI without Python or torch: examples/c_host/step_loop (C++, HIP
+    runtime + libmarlnav.so) initialises the envs (marlnav_reinit_all), steps
+    them with the given actions (marlnav_step per step, the native re-init
+    keyed by the step index) and sums the counters; the Python Env with the
+    same dims, parameters, seed and actions ends bit for bit in the same
+    state, last outputs and counters (5-step episodes: re-inits happen)."""
+    exe = os.path.join(ROOT, "examples", "c_host", "step_loop")
+    assert os.path.exists(exe), "examples/c_host/step_loop not built (__graft_entry__.build)"
+    env = make_env(pkg, P, A, O, episode_len=5, seed=2024,
+                   factors=dict(risk_factor=2., distance_factor=3., bond_factor=5.))
+    env._sync_params()
+    acts = ((np.random.default_rng(P + A).random((steps, P, A, 2), dtype=np.float32) - 0.5)
+            * np.float32(0.8)).astype(np.float32)
+    inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
+    with open(inp, "wb") as f:
+        f.write(bytes(env._dims))
+        f.write(bytes(env._cparams))
+        f.write(np.int32(steps).tobytes())
+        f.write(np_(env._formation).astype(np.float32).tobytes())
+        f.write(acts.tobytes())
+    r = subprocess.run([exe, str(inp), str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for k in range(steps):
+        obs, rew, term, trunc = env.step(torch.from_numpy(acts[k]).to(DEV))
+    torch.cuda.synchronize()
+    D = 2 + 2 * O + 2 * (A - 1)
+    raw = out.read_bytes()
+    parts = [("states", np.float32, (P, A, 5), env.states), ("obstacles", np.float32, (P, O, 2), env.obstacles),
+             ("target", np.float32, (P, 1, 2), env.target), ("step_num", np.float32, (P,), env._step_num),
+             ("terminates", np.uint8, (P,), env._terminates), ("obs", np.float32, (P, A, D), obs._packed),
+             ("reward", np.float32, (P,), rew), ("terminated", np.uint8, (P,), term),
+             ("truncated", np.uint8, (P,), trunc)]
+    off = 0
+    for name, dt, shape, got in parts:
+        n = int(np.prod(shape)) * np.dtype(dt).itemsize
+        c = np.frombuffer(raw[off:off + n], dtype=dt).reshape(shape)
+        off += n
+        g = np_(got)
+        g = g.astype(np.uint8) if dt == np.uint8 else g
+        assert g.shape == c.shape, (name, g.shape, c.shape)
+        np.testing.assert_array_equal(g.view(np.uint32) if dt == np.float32 else g,
+                                      c.view(np.uint32) if dt == np.float32 else c, name)
+    counters = np.frombuffer(raw[off:off + 24], dtype=np.uint64)
+    assert off + 24 == len(raw)
+    assert tuple(int(x) for x in counters) == (env._num_trunc, env._num_col, env._num_tar)
+    assert counters[0] > 0  # the 5-step episodes truncated
