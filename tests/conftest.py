@@ -106,6 +106,36 @@ def assert_vec_close(a, e, rtol=RTOL, atol=0.0, what=""):
     assert not bad.any(), _report(what, a, e, bad)
 
 
+# (test, compared against, angle entries, entries that needed the absolute
+# floor, worst relative error where |angle| > 1e-3), filled by
+# record_angle_stats and printed in the session summary
+ANGLE_STATS = []
+
+
+def record_angle_stats(test, against, actual_fields, expected_fields):
+    n_floor, worst = angle_error_stats(actual_fields, expected_fields)
+    n = sum(int(np.asarray(a).size) for f, a in zip(OBS_FIELDS, actual_fields)
+            if f in ANGLE_FIELDS)
+    ANGLE_STATS.append((test, against, n, n_floor, worst))
+    return n_floor, worst
+
+
+def pytest_terminal_summary(terminalreporter):
+    if not ANGLE_STATS:
+        return
+    agg = {}
+    for test, against, n, n_floor, worst in ANGLE_STATS:
+        a = agg.setdefault((test, against), [0, 0, 0.0])
+        a[0] += n
+        a[1] += n_floor
+        a[2] = max(a[2], worst)
+    tr = terminalreporter
+    tr.write_sep("-", "angle fields: entries within ANGLE_ATOL only, worst relative error")
+    for (test, against), (n, n_floor, worst) in sorted(agg.items()):
+        tr.write_line(f"{test} vs {against}: {n} angles, {n_floor} needed the "
+                      f"{ANGLE_ATOL:g} floor, worst rel err {worst:.3g} (|angle| > 1e-3)")
+
+
 def angle_error_stats(actual_fields, expected_fields):
     """(entries needing the absolute floor, worst relative error) over the
     angle fields - reported by the tests so the ANGLE_ATOL floor's use is

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import (ANGLE_ATOL, OBS_FIELDS, ROOT, RTOL, assert_obs_close,
+from conftest import (ANGLE_ATOL, OBS_FIELDS, ROOT, RTOL, assert_obs_close, record_angle_stats,
                       assert_states_close, assert_vec_close, cli_args, env_values, golden, meta)
 
 import oracle as orc
@@ -82,6 +82,8 @@ def test_step_matches_reference_golden(pkg, name):
         assert_states_close(np_(env.states), z["out_states"][k], where)
         assert_obs_close(fields_np(obs), {f: z["obs_" + f][k] for f in OBS_FIELDS},
                          prefix="", where=where)
+        record_angle_stats("golden F1", "reference", fields_np(obs),
+                           [z["obs_" + f][k] for f in OBS_FIELDS])
         f0 = fields_np(obs0)
         for f, a in zip(OBS_FIELDS, f0):
             if "distance" in f:  # correctly rounded sqrt: bit-exact
@@ -123,6 +125,7 @@ def test_step_bit_exact_vs_oracle(pkg, name):
             if "distance" in f:
                 np.testing.assert_array_equal(a, e, where + " " + f)
         assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, exact_distances=True, where=where)
+        record_angle_stats("golden F1 inputs", "oracle", fg, fo)
 
 
 def _trace_env(pkg, name):
@@ -156,6 +159,8 @@ def test_trace_matches_reference(pkg, name):
         assert_vec_close(np_(rew), z["reward"][k], what=where + " reward")
         assert_obs_close(fields_np(obs), {f: z["obs_" + f][k] for f in OBS_FIELDS},
                          prefix="", where=where)
+        record_angle_stats(f"trace {name}", "reference", fields_np(obs),
+                           [z["obs_" + f][k] for f in OBS_FIELDS])
         if k % 100 == 99:
             assert (env._num_trunc, env._num_col, env._num_tar) == (
                 z["num_trunc"][k], z["num_col"][k], z["num_tar"][k]), where

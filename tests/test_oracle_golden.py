@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import (OBS_FIELDS, assert_obs_close, assert_states_close, assert_traj_obs_close,
+from conftest import (OBS_FIELDS, assert_obs_close, record_angle_stats, assert_states_close, assert_traj_obs_close,
                       assert_vec_close, cli_args, env_values, golden, meta)
 
 import oracle as orc
@@ -53,6 +53,8 @@ def test_oracle_step_matches_reference(name, mk):
         fields = orc.split_obs(o["obs"], A, O)
         assert_obs_close(fields, {f: z["obs_" + f][k] for f in OBS_FIELDS}, prefix="",
                          where=where)
+        record_angle_stats("oracle F1", "reference", fields,
+                           [z["obs_" + f][k] for f in OBS_FIELDS])
     assert np.mean(exact_rewards) > 0.95   # nearly all bit for bit
 
 
@@ -140,6 +142,8 @@ def test_oracle_trace_matches_reference(name, pkg, mk):
         fields = orc.split_obs(o["obs"], A, O)
         assert_obs_close(fields, {f: z["obs_" + f][k] for f in OBS_FIELDS}, prefix="",
                          where=where)
+        record_angle_stats(f"oracle trace {name}", "reference", fields,
+                           [z["obs_" + f][k] for f in OBS_FIELDS])
 
 
 def test_config1_known_answers():
