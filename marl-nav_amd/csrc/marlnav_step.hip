@@ -237,9 +237,14 @@ constexpr int64_t kSplitTinyWaves = 256;
 #undef MARLNAV_SPLIT_VARIANT
 
 // one-lane-per-row grids below kSplitBelowWaves * (pairs per row / 6) waves
-// leave most SIMDs idle (measured: 4096x3x3 and 16384x3x8 split faster,
-// 16384x3x3 does not)
+// leave most SIMDs idle (measured: 16384x3x8 split faster, 16384x3x3 not)
 constexpr int64_t kSplitBelowWaves = 512;
+// ... except that with at most 6 pairs per row (A3/O3) the env-block kernel is
+// faster from one full block of 64 envs on (graph replay, round 2, with
+// kernarg preload: 64x3x3 4.20 vs 4.28 us, 1024x3x3 5.23 vs 5.37, 4096x3x3
+// 5.41 vs 5.59, 8192x3x3 5.51 vs 6.10; 32x3x3 4.05 vs 5.05 stays split;
+// profiles/r02_family_ab.txt)
+constexpr int64_t kBlockFromEnvs = 64;
 
 const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only,
                                  bool force_size = false)
@@ -258,6 +263,8 @@ const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers 
     const int64_t row_waves = (d->num_parallel + tile_envs(v->A) - 1) / tile_envs(v->A);
     const int64_t pairs = 1 + v->O + (v->A - 1);
     if (!v->always && !force_size && row_waves * 6 >= kSplitBelowWaves * pairs)
+        return nullptr;
+    if (!v->always && !force_size && pairs <= 6 && d->num_parallel >= kBlockFromEnvs)
         return nullptr;
     if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
         !aligned(b.obs, 16))

@@ -492,7 +492,7 @@ def test_extreme_coordinates_take_the_exact_path(pkg, P, A, O):
                                             "terminates"))
 
 
-@pytest.mark.parametrize("P,A,O", [(20000 + 13, 3, 3), (8192 + 5, 3, 8), (300, 3, 3)])
+@pytest.mark.parametrize("P,A,O", [(20000 + 13, 3, 3), (8192 + 5, 3, 8), (300, 3, 3), (60, 3, 3)])
 def test_reference_rng_fresh_candidates_bit_exact_vs_oracle(pkg, P, A, O):
     """rng='reference' at block-kernel sizes (and one split-kernel size):
     finished envs take the host's fresh candidates (environment.py:76-90
@@ -656,7 +656,7 @@ def test_reward_term_divisions_bit_exact_for_any_parameters(pkg, geom, shape):
                                                "terminates"))
 
 
-@pytest.mark.parametrize("P,A,O", [(4096 + 7, 3, 3), (300, 3, 3), (512, 16, 32)])
+@pytest.mark.parametrize("P,A,O", [(4096 + 7, 3, 3), (300, 3, 3), (60, 3, 3), (512, 16, 32)])
 def test_non_finite_inputs_match_oracle(pkg, P, A, O):
     """NaN / inf actions and state entries propagate exactly as in the oracle
     (torch.clamp passes NaN, comparisons with NaN are false): states, rewards
@@ -760,7 +760,7 @@ def _run_vs_oracle(env, dm, pr, st, ob, tg, sn, te, acts_list, form=None, fresh_
     return st, ob, tg, sn, te
 
 
-@pytest.mark.parametrize("P,A,O", [(4096 + 7, 3, 3), (300, 3, 3), (2048, 3, 8), (512, 16, 32),
+@pytest.mark.parametrize("P,A,O", [(4096 + 7, 3, 3), (300, 3, 3), (60, 3, 3), (2048, 3, 8), (512, 16, 32),
                                    (777, 5, 2)])
 def test_non_finite_env_reinitialised_like_the_reference_blend(pkg, P, A, O):
     """_reinit_update (environment.py:86-90) is 0*old + 1*fresh for a
@@ -788,7 +788,7 @@ def test_non_finite_env_reinitialised_like_the_reference_blend(pkg, P, A, O):
                    np.zeros(P, np.bool_), acts, form=form, where=f"P{P} A{A} O{O}")
 
 
-@pytest.mark.parametrize("P,A,O", [(20000 + 13, 3, 3), (300, 3, 3), (512, 16, 32)])
+@pytest.mark.parametrize("P,A,O", [(20000 + 13, 3, 3), (300, 3, 3), (60, 3, 3), (512, 16, 32)])
 def test_reference_rng_non_finite_fresh_candidates(pkg, P, A, O):
     """Reference-RNG mode with a sampler that returns NaN/inf candidates:
     the reference's blend makes a KEPT env's value NaN too (1*old +
