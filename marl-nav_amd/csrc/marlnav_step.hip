@@ -205,6 +205,10 @@ const KernelPair kVariants[] = {
 // (kHotKargsOff, kernel_args.h), then KArgs
 using BlockFn = void (*)(float *, const float *, const float *, const float *, const float *,
                          const uint8_t *, int64_t, KArgs);
+// the kernarg layout places each argument at its natural alignment: six
+// pointers and an int64 (56 bytes), then KArgs - where kargs_late reads it
+static_assert(6 * sizeof(float *) + sizeof(int64_t) == kHotKargsOff && alignof(KArgs) <= 8,
+              "KArgs must follow the seven preloaded arguments at kHotKargsOff");
 
 bool aligned(const void *p, uintptr_t n) { return (reinterpret_cast<uintptr_t>(p) & (n - 1)) == 0; }
 
