@@ -388,6 +388,26 @@ __global__ void __launch_bounds__(64 * A)
     if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
                                                st, tid);  // (E = 64: whole 16-byte pieces)
+    } else if (!OBS_ONLY && full && NT % D == 0) {
+        // ---- the same with the fused ObsNormalizer (utils.py:519-532):
+        // thread tid only ever meets feature tid % D (NT is a multiple of D),
+        // so its mean and scale are loaded once; every LDS read and every
+        // division is issued ahead of the stores
+        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
+                                               st, tid);
+        KArgsK *kl = kargs_late<kHotKargsOff>();
+        const int kk = tid % D;
+        const float m = kl->a.b.norm_mean[kk], sc = kl->a.b.norm_scale[kk];
+        float *gn = kl->a.b.obs_norm + e0 * (A * D);
+        constexpr int K = E * A * D / NT;
+        static_assert(E * A * D % NT == 0, "whole passes");
+        float v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = obs_rows[tid + k * NT];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = (v[k] - m) / sc;
+#pragma unroll
+        for (int k = 0; k < K; ++k) out_st<kNtRows>(gn + tid + k * NT, v[k]);
     } else if (!OBS_ONLY) {
         block_store(gobs, obs_rows, nrow * D, tid, NT);
         if (norm) {
