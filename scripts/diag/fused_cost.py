@@ -24,8 +24,19 @@ for mode in ("plain", "norm", "scale", "norm+scale"):
         env.attach_normalizer(pkg.ObsNormalizer(pkg.set_normalizer_params(args, dev)))
     if "scale" in mode:
         env.attach_action_scaler(pkg.ActionScaler(pkg.set_scaler_params(args, dev)))
+    # the Python step loop as MAPPO drives it (host engine; timed like bench.py)
+    import time
+    for i in range(20):
+        env.step(acts[i % 8])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(500):
+        env.step(acts[i % 8])
+    torch.cuda.synchronize()
+    loop_us = (time.perf_counter() - t0) * 1e6 / 500
     mean, med = bench.kernel_time_us(env, acts)
-    print(f"{P}x3x3 {mode}: graph-replay step {mean:.2f}/{med:.2f} us mean/median", flush=True)
+    print(f"{P}x3x3 {mode}: graph-replay step {mean:.2f}/{med:.2f} us mean/median, "
+          f"Python Env.step loop {loop_us:.2f} us/step", flush=True)
     del env
 # unfused: the step, then the normaliser as torch ops on the packed obs
 env = bench.make_env(pkg, P, 3, 3, dev, 0, seed=20251004)
