@@ -411,12 +411,21 @@ __global__ void __launch_bounds__(64 * A)
     } else if (!OBS_ONLY) {
         block_store(gobs, obs_rows, nrow * D, tid, NT);
         if (norm) {
+            // mean and scale staged in LDS once (the reward-term slots are
+            // free after the per-env phase), then one pass over the rows
             KArgsK *kl = kargs_late<kHotKargsOff>();
-            const float *mean = kl->a.b.norm_mean, *scale = kl->a.b.norm_scale;
+            float *ms = lds + BP::RED;
+            static_assert(4 * R >= 2 * D, "mean and scale fit the reward-term slots");
+            if (tid < D) {
+                ms[tid] = kl->a.b.norm_mean[tid];
+                ms[D + tid] = kl->a.b.norm_scale[tid];
+            }
+            __syncthreads();
             float *gn = kl->a.b.obs_norm + e0 * (A * D);
+#pragma unroll 4
             for (int i = tid; i < nrow * D; i += NT) {
                 const int kk = i % D;
-                gn[i] = (obs_rows[i] - mean[kk]) / scale[kk];
+                gn[i] = (obs_rows[i] - ms[kk]) / ms[D + kk];
             }
         }
         block_store(in_sgpr(b.states + e0 * (A * 5)), st, nrow * 5, tid, NT);
