@@ -745,6 +745,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             for (int i = (int)lane; i < n; i += 64) out_st<kNtRows>(gobs + i, src[i]);
         }
         if (gnorm)
+#pragma unroll 8  // (mean/scale loads of 8 iterations in flight at once)
             for (int i = (int)lane; i < n; i += 64) {
                 const int rr = i / D, kk = i - rr * D;
                 gnorm[i] = (src[rr * SP::DP + kk] - mean[kk]) / scale[kk];

@@ -1093,3 +1093,26 @@ def test_c_host_matches_python_env(pkg, P, A, O, steps, tmp_path):
     assert off + 24 == len(raw)
     assert tuple(int(x) for x in counters) == (env._num_trunc, env._num_col, env._num_tar)
     assert counters[0] > 0  # the 5-step episodes truncated
+
+
+@pytest.mark.parametrize("P,A,O", [(4096, 3, 3), (2048 + 5, 3, 8), (60, 3, 3), (512, 16, 32)])
+def test_fused_normalizer_every_store_path(pkg, P, A, O):
+    """The fused normaliser (MARLNAV_WRITE_OBS_NORM, utils.py:519-532) in
+    every store path: the env-block kernel's per-thread-feature path (A3/O3
+    full blocks), its generic path (A3/O8: D does not divide the block), the
+    pair-split kernel (LPR 8 at 60 envs, A16/O32): the fused output equals
+    (obs - mean) / scale in torch bit for bit, with a mean and scale per
+    feature (re-inits included: 4-step episodes)."""
+    from types import SimpleNamespace
+    D = 2 + 2 * O + 2 * (A - 1)
+    g = torch.Generator().manual_seed(P + D)
+    mean = (torch.rand(D, generator=g) * 100 - 50).to(DEV)
+    scale = (torch.rand(D, generator=g) * 900 + 0.5).to(DEV)
+    env = make_env(pkg, P, A, O, episode_len=4, seed=7)
+    env.attach_normalizer(SimpleNamespace(mean=mean, scale=scale))
+    for k in range(6):
+        acts = ((torch.rand(P, A, 2, generator=g) - 0.5) * 0.8).to(DEV)
+        obs, rew, term, trunc = env.step(acts)
+        ref = (obs._packed - mean) / scale
+        torch.testing.assert_close(obs._normalized, ref, rtol=0, atol=0,
+                                   msg=f"P{P} A{A} O{O} step {k + 1}")
