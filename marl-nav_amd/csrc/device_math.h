@@ -51,13 +51,13 @@ __device__ __forceinline__ void out_st2(float *p, float2 v)
         *reinterpret_cast<float2 *>(p) = v;
 }
 
-// Fast-path switches for the pair math in FAST mode: 1 = the shortened
-// sequence (bit-exact inside its guard, scripts/probes/fastmath_probe.hip),
-// 0 = the IEEE operation. The tile kernels enter FAST mode only for a wave
-// whose every coordinate passed coords_in_range() (which implies every
-// per-pair guard), so there the guards are dead code. Kernels that evaluate
-// the guards per pair (wave/split kernels) were measured slower with them and
-// run IEEE-only (kGuardedFast).
+// The pair math's FAST mode (the shortened sequences, bit-exact inside their
+// guards: scripts/probes/fastmath_probe.hip, sqrt_probe.hip) is entered only
+// for a block or tile whose every coordinate passed the coordinate check
+// (CoordRange / tile_coords_ok), which implies every per-pair guard, so
+// there the guards are dead code. The generic wave kernel, which would have
+// to evaluate the guards per pair, was measured slower with them and runs
+// IEEE-only (kGuardedFast).
 constexpr bool kGuardedFast = false;
 // Internal MarlnavParams.flags bit set by marlnav_step when every reward
 // parameter lies inside the short division sequences' guards

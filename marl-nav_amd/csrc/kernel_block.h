@@ -5,13 +5,14 @@
 
 // ------------------------------------------------------- env-block kernel
 // One workgroup of A waves per block of E = 64 consecutive envs: lane l of
-// wave w owns agent w of env l. Every lane holds a row (the tile kernels
-// leave 64 - 3*20 = 4 lanes idle at A3), the agent index is wave-uniform, and
-// the per-env phase runs once per block on wave 0 with all 64 lanes busy
-// instead of on 20 of 64 lanes in every wave. Grid shape: at 65536 envs x 3
-// agents, 1024 blocks of 3 waves = 3 waves on every SIMD, where 64/3-env
-// wave tiles give 3277 waves and a fifth of the SIMDs a fourth wave (measured
-// by scripts/kstamps.py: those SIMDs set the kernel's end).
+// wave w owns agent w of env l. Every lane holds a row (wave tiles of whole
+// envs - the round-1 tile family - left 64 - 3*20 = 4 lanes idle at A3), the
+// agent index is wave-uniform, and the per-env phase runs once per block on
+// wave 0 with all 64 lanes busy instead of on 20 of 64 lanes in every wave.
+// Grid shape: at 65536 envs x 3 agents, 1024 blocks of 3 waves = 3 waves on
+// every SIMD, where 64/3-env wave tiles give 3277 waves and a fifth of the
+// SIMDs a fourth wave (measured by scripts/kstamps.py: those SIMDs set the
+// kernel's end).
 // Rows are exchanged through LDS between block barriers (5 per step); the
 // packed observation rows are assembled in LDS and streamed out as one
 // contiguous span (a store instruction covers 1 KiB, 8 cache lines, where

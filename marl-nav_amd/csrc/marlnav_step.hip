@@ -300,8 +300,7 @@ int launch_split(const SplitVariant &v, BlockFn fn, const StepArgs &args, const 
     return 0;
 }
 
-// env-block kernels (block_kernel) for these shapes; MARLNAV_BLOCK=0 turns
-// them off (A/B timing against the tile kernels)
+// env-block kernels (block_kernel) for these shapes
 struct BlockVariant {
     int A, O;
     BlockFn step, obs, noisy;
