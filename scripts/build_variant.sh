@@ -17,6 +17,6 @@ if [ -n "$rev" ]; then
 fi
 cd "$src/marl-nav_amd/csrc"
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -ffp-contract=off \
-    -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp -Wno-pass-failed "$@" marlnav_step.hip marlnav_rollout.hip -o "$ROOT/marl-nav_amd/lib/$name.so"
+    -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp -mllvm -amdgpu-kernarg-preload-count=14 -Wno-pass-failed "$@" marlnav_step.hip marlnav_rollout.hip -o "$ROOT/marl-nav_amd/lib/$name.so"
 [ -n "$tmp" ] && rm -rf "$tmp"
 echo "built marl-nav_amd/lib/$name.so"
