@@ -97,7 +97,34 @@ struct Engine {
     std::vector<OutSet *> *pool;
     int next;
     OutSet *last;                 // the set the previous step returned
+    // the Env's obstacles / target tensors (strong refs, track_state): a
+    // step may not write them in place while anything else refers to them
+    PyObject *held[2];
+    c10::Storage held_st[2];
 };
+
+// The reference never writes `obstacles` / `target` in place: its re-init
+// rebinds them to new tensors (environment.py:79-81), so a caller holding
+// the old tensor keeps the pre-step values. Here the step kernel re-
+// initialises finished envs in place, so the step goes through Env._step_py,
+// which gives the Env fresh copies first, whenever a tensor is referenced
+// beyond the Env's attribute and this engine (2 Python references) or its
+// storage is viewed by another tensor (use count beyond the tensor's own and
+// this engine's copy).
+bool state_shared(const Engine *e, int i)
+{
+    return e->held[i] && (Py_REFCNT(e->held[i]) > 2 || e->held_st[i].use_count() > 2);
+}
+
+bool any_state_shared(const Engine *e) { return state_shared(e, 0) || state_shared(e, 1); }
+
+void release_state(Engine *e)
+{
+    for (int i = 0; i < 2; ++i) {
+        Py_CLEAR(e->held[i]);
+        e->held_st[i] = c10::Storage();
+    }
+}
 
 PyObject *raise_step_error(Engine *e, int rc)
 {
@@ -322,6 +349,9 @@ int Engine_init(Engine *e, PyObject *args, PyObject *)
     e->steps_done = 0;
     e->next = 0;
     e->last = nullptr;
+    e->held[0] = e->held[1] = nullptr;
+    new (&e->held_st[0]) c10::Storage();
+    new (&e->held_st[1]) c10::Storage();
     return e->dev_index ? 0 : -1;
 }
 
@@ -329,6 +359,9 @@ void Engine_dealloc(Engine *e)
 {
     clear_pool(e);
     delete e->pool;
+    release_state(e);
+    e->held_st[0].~Storage();
+    e->held_st[1].~Storage();
     Py_CLEAR(e->stream_fn);
     Py_CLEAR(e->dev_index);
     Py_CLEAR(e->factory);
@@ -381,7 +414,7 @@ PyObject *Engine_call(Engine *e, PyObject *args, PyObject *kw)
         return nullptr;
     }
     a = PyTuple_GET_ITEM(args, 0);
-    if (e->fast_ok && THPVariable_Check(a)) {
+    if (e->fast_ok && !any_state_shared(e) && THPVariable_Check(a)) {
         const at::Tensor &t = THPVariable_Unpack(a);
         if (t.scalar_type() == at::kFloat && t.dim() == 3 && t.is_cuda() &&
             t.get_device() == e->device && t.size(0) == e->act_shape[0] &&
@@ -412,6 +445,32 @@ PyObject *Engine_launch(Engine *e, PyObject *args)
         fp = &f;
     }
     return do_launch(e, (const void *)act, fp, extra);
+}
+
+// track_state(obstacles, target): the Env's current tensors
+PyObject *Engine_track_state(Engine *e, PyObject *args)
+{
+    PyObject *o[2];
+    if (!PyArg_ParseTuple(args, "OO", &o[0], &o[1])) return nullptr;
+    for (int i = 0; i < 2; ++i)
+        if (!THPVariable_Check(o[i])) {
+            PyErr_SetString(PyExc_TypeError, "track_state(obstacles, target): tensors");
+            return nullptr;
+        }
+    release_state(e);
+    for (int i = 0; i < 2; ++i) {
+        Py_INCREF(o[i]);
+        e->held[i] = o[i];
+        e->held_st[i] = THPVariable_Unpack(o[i]).storage();
+    }
+    Py_RETURN_NONE;
+}
+
+// (obstacles_shared, target_shared)
+PyObject *Engine_shared_state(Engine *e, PyObject *)
+{
+    return Py_BuildValue("(OO)", state_shared(e, 0) ? Py_True : Py_False,
+                         state_shared(e, 1) ? Py_True : Py_False);
 }
 
 PyObject *Engine_reset_pool(Engine *e, PyObject *)
@@ -445,6 +504,10 @@ PyMethodDef Engine_methods[] = {
     {"launch", (PyCFunction)Engine_launch, METH_VARARGS,
      "launch(actions_ptr, fresh_ptrs|None, extra_flags) -> (obs, reward, terminated, truncated)"},
     {"reset_pool", (PyCFunction)Engine_reset_pool, METH_NOARGS, "drop every pooled output set"},
+    {"track_state", (PyCFunction)Engine_track_state, METH_VARARGS,
+     "track_state(obstacles, target): the tensors a step must not write while shared"},
+    {"shared_state", (PyCFunction)Engine_shared_state, METH_NOARGS,
+     "(obstacles_shared, target_shared)"},
     {"last_finished", (PyCFunction)Engine_last_finished, METH_NOARGS,
      "(terminated, truncated) of the last step or None"},
     {"pool_info", (PyCFunction)Engine_pool_info, METH_NOARGS, "[(obs_ptr, free)] per pooled set"},

@@ -10,8 +10,13 @@ synchronises with the host.
 
 Differences from the reference, all deliberate:
 
-* ``states``/``obstacles``/``target`` are device buffers updated in place by
-  each step (the reference rebinds them to new tensors); clone to snapshot.
+* ``states`` is a device buffer updated in place by each step. The reference
+  also moves it in place (environment.py:113-123) but rebinds it to a new
+  tensor at the re-init (:79), so a caller holding the pre-step tensor sees
+  the moved values there and here, and here also the finished envs' fresh
+  values; clone to snapshot. ``obstacles`` / ``target`` are copied on write:
+  a step never changes a tensor referenced outside the Env (the reference
+  only rebinds them).
 * The episode counters live on the device; reading one synchronises.
 * ``env.step`` is the native host engine (``abi.load_host()``, C++): it
   checks the actions, picks the output tensors and enqueues the kernel
@@ -256,6 +261,21 @@ class Env(object):
         fast = (not self._params_dirty and self._rng == 'native'
                 and self._init_sampler is self._default_init_sampler)
         eng.configure(bytes(self._dims), bytes(self._cparams), bytes(b), fast)
+        eng.track_state(self._obstacles, self._target)
+
+    def _unshare_state(self):
+        """Copy-on-write of `obstacles` / `target`: the reference's re-init
+        rebinds them to new tensors (environment.py:79-81) and never writes
+        them in place, so a caller still holding the tensor from before a step
+        keeps its values. The kernel re-initialises finished envs in place;
+        when the engine reports a tensor referenced outside the Env, the Env
+        moves to a copy (stream-ordered) before the step writes."""
+        ob_shared, tg_shared = self._engine.shared_state()
+        if ob_shared:
+            object.__setattr__(self, '_obstacles', self._obstacles.clone())
+        if tg_shared:
+            object.__setattr__(self, '_target', self._target.clone())
+        self._configure()
 
     def _slots(self):
         n = self._lib.marlnav_counter_slots(ctypes.byref(self._dims))
@@ -532,6 +552,8 @@ class Env(object):
         modes (the host init sampler is called every step, environment.py:78)."""
         if self._params_dirty:
             self._sync_params()
+        if any(self._engine.shared_state()):
+            self._unshare_state()
         dev = self.device
         if not (type(actions) is torch.Tensor and actions.dtype is _F32
                 and actions.device == dev and actions.shape == self._act_shape

@@ -352,6 +352,42 @@ def test_step_outputs_never_alias_live_tensors(pkg):
     assert len(ptrs) <= 4
 
 
+def test_held_obstacles_and_target_are_copied_on_write(pkg):
+    """The reference never writes obstacles / target in place (its re-init
+    rebinds them, environment.py:79-81): a caller holding the pre-step tensor,
+    or a view of it, keeps its values here too. Nothing held: the step writes
+    the Env's buffers in place (no copies). Holders change nothing else: the
+    trajectory equals one run without holders, bit for bit."""
+    P = 4096 + 7
+    env = make_env(pkg, P, 3, 3, episode_len=3)   # every env truncates at step 3
+    twin = make_env(pkg, P, 3, 3, episode_len=3)
+    acts = [torch.rand(P, 3, 2, device=DEV) - 0.5 for _ in range(3)]
+    p_ob, p_tg = env.obstacles.data_ptr(), env.target.data_ptr()
+    for k in range(4):
+        env.step(acts[k % 3])
+        twin.step(acts[k % 3])
+    assert (env.obstacles.data_ptr(), env.target.data_ptr()) == (p_ob, p_tg)
+    ob, tg_view = env.obstacles, env.target[:, 0]
+    ob0, tg0 = ob.clone(), tg_view.clone()
+    for k in range(4, 8):
+        o1 = env.step(acts[k % 3])[0]
+        o2 = twin.step(acts[k % 3])[0]
+        assert torch.equal(o1._packed, o2._packed)
+    torch.cuda.synchronize()
+    assert torch.equal(ob, ob0) and torch.equal(tg_view, tg0)
+    assert env.obstacles.data_ptr() != p_ob and env.target.data_ptr() != p_tg
+    assert not torch.equal(env.obstacles, ob0)    # its own buffer was re-initialised
+    for a, b in ((env.states, twin.states), (env.obstacles, twin.obstacles),
+                 (env.target, twin.target)):
+        assert torch.equal(a, b)
+    # holders gone (the loop's names too): back to in-place steps
+    del ob, tg_view, a, b
+    q_ob, q_tg = env.obstacles.data_ptr(), env.target.data_ptr()
+    for k in range(3):
+        env.step(acts[k])
+    assert (env.obstacles.data_ptr(), env.target.data_ptr()) == (q_ob, q_tg)
+
+
 def test_discounted_returns_match_reference_and_oracle(pkg):
     """§8(f) row 3: the device scan against MAPPO._process_rewards run
     unmodified (F5) and the C oracle at rollout size; float64 within 1e-12."""
