@@ -97,30 +97,34 @@ struct Engine {
     std::vector<OutSet *> *pool;
     int next;
     OutSet *last;                 // the set the previous step returned
-    // the Env's obstacles / target tensors (strong refs, track_state): a
-    // step may not write them in place while anything else refers to them
-    PyObject *held[2];
-    c10::Storage held_st[2];
+    // the Env's states / obstacles / target tensors (strong refs,
+    // track_state): a step may not write them in place while anything else
+    // refers to them
+    PyObject *held[3];
+    c10::Storage held_st[3];
 };
 
-// The reference never writes `obstacles` / `target` in place: its re-init
-// rebinds them to new tensors (environment.py:79-81), so a caller holding
-// the old tensor keeps the pre-step values. Here the step kernel re-
-// initialises finished envs in place, so the step goes through Env._step_py,
-// which gives the Env fresh copies first, whenever a tensor is referenced
-// beyond the Env's attribute and this engine (2 Python references) or its
-// storage is viewed by another tensor (use count beyond the tensor's own and
-// this engine's copy).
+// The reference's re-init rebinds `states`, `obstacles` and `target` to new
+// tensors (environment.py:79-81), so a caller holding the old tensor keeps
+// its pre-re-init values (for `states`: the moved ones, :113-123 move in
+// place). Here the step kernel writes them in place, so the step goes
+// through Env._step_py, which gives the Env fresh copies first, whenever a
+// tensor is referenced beyond the Env's attribute and this engine (2 Python
+// references) or its storage is viewed by another tensor (use count beyond
+// the tensor's own and this engine's copy).
 bool state_shared(const Engine *e, int i)
 {
     return e->held[i] && (Py_REFCNT(e->held[i]) > 2 || e->held_st[i].use_count() > 2);
 }
 
-bool any_state_shared(const Engine *e) { return state_shared(e, 0) || state_shared(e, 1); }
+bool any_state_shared(const Engine *e)
+{
+    return state_shared(e, 0) || state_shared(e, 1) || state_shared(e, 2);
+}
 
 void release_state(Engine *e)
 {
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         Py_CLEAR(e->held[i]);
         e->held_st[i] = c10::Storage();
     }
@@ -349,9 +353,10 @@ int Engine_init(Engine *e, PyObject *args, PyObject *)
     e->steps_done = 0;
     e->next = 0;
     e->last = nullptr;
-    e->held[0] = e->held[1] = nullptr;
-    new (&e->held_st[0]) c10::Storage();
-    new (&e->held_st[1]) c10::Storage();
+    for (int i = 0; i < 3; ++i) {
+        e->held[i] = nullptr;
+        new (&e->held_st[i]) c10::Storage();
+    }
     return e->dev_index ? 0 : -1;
 }
 
@@ -360,8 +365,7 @@ void Engine_dealloc(Engine *e)
     clear_pool(e);
     delete e->pool;
     release_state(e);
-    e->held_st[0].~Storage();
-    e->held_st[1].~Storage();
+    for (int i = 0; i < 3; ++i) e->held_st[i].~Storage();
     Py_CLEAR(e->stream_fn);
     Py_CLEAR(e->dev_index);
     Py_CLEAR(e->factory);
@@ -447,18 +451,18 @@ PyObject *Engine_launch(Engine *e, PyObject *args)
     return do_launch(e, (const void *)act, fp, extra);
 }
 
-// track_state(obstacles, target): the Env's current tensors
+// track_state(states, obstacles, target): the Env's current tensors
 PyObject *Engine_track_state(Engine *e, PyObject *args)
 {
-    PyObject *o[2];
-    if (!PyArg_ParseTuple(args, "OO", &o[0], &o[1])) return nullptr;
-    for (int i = 0; i < 2; ++i)
+    PyObject *o[3];
+    if (!PyArg_ParseTuple(args, "OOO", &o[0], &o[1], &o[2])) return nullptr;
+    for (int i = 0; i < 3; ++i)
         if (!THPVariable_Check(o[i])) {
-            PyErr_SetString(PyExc_TypeError, "track_state(obstacles, target): tensors");
+            PyErr_SetString(PyExc_TypeError, "track_state(states, obstacles, target): tensors");
             return nullptr;
         }
     release_state(e);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         Py_INCREF(o[i]);
         e->held[i] = o[i];
         e->held_st[i] = THPVariable_Unpack(o[i]).storage();
@@ -466,11 +470,12 @@ PyObject *Engine_track_state(Engine *e, PyObject *args)
     Py_RETURN_NONE;
 }
 
-// (obstacles_shared, target_shared)
+// (states_shared, obstacles_shared, target_shared)
 PyObject *Engine_shared_state(Engine *e, PyObject *)
 {
-    return Py_BuildValue("(OO)", state_shared(e, 0) ? Py_True : Py_False,
-                         state_shared(e, 1) ? Py_True : Py_False);
+    return Py_BuildValue("(OOO)", state_shared(e, 0) ? Py_True : Py_False,
+                         state_shared(e, 1) ? Py_True : Py_False,
+                         state_shared(e, 2) ? Py_True : Py_False);
 }
 
 PyObject *Engine_reset_pool(Engine *e, PyObject *)
@@ -505,9 +510,9 @@ PyMethodDef Engine_methods[] = {
      "launch(actions_ptr, fresh_ptrs|None, extra_flags) -> (obs, reward, terminated, truncated)"},
     {"reset_pool", (PyCFunction)Engine_reset_pool, METH_NOARGS, "drop every pooled output set"},
     {"track_state", (PyCFunction)Engine_track_state, METH_VARARGS,
-     "track_state(obstacles, target): the tensors a step must not write while shared"},
+     "track_state(states, obstacles, target): the tensors a step must not write while shared"},
     {"shared_state", (PyCFunction)Engine_shared_state, METH_NOARGS,
-     "(obstacles_shared, target_shared)"},
+     "(states_shared, obstacles_shared, target_shared)"},
     {"last_finished", (PyCFunction)Engine_last_finished, METH_NOARGS,
      "(terminated, truncated) of the last step or None"},
     {"pool_info", (PyCFunction)Engine_pool_info, METH_NOARGS, "[(obs_ptr, free)] per pooled set"},

@@ -10,13 +10,13 @@ synchronises with the host.
 
 Differences from the reference, all deliberate:
 
-* ``states`` is a device buffer updated in place by each step. The reference
-  also moves it in place (environment.py:113-123) but rebinds it to a new
-  tensor at the re-init (:79), so a caller holding the pre-step tensor sees
-  the moved values there and here, and here also the finished envs' fresh
-  values; clone to snapshot. ``obstacles`` / ``target`` are copied on write:
-  a step never changes a tensor referenced outside the Env (the reference
-  only rebinds them).
+* ``states``/``obstacles``/``target`` are device buffers the step kernel
+  writes in place. When a caller holds one (or a view), the step first moves
+  the Env to a copy, so the holder sees what it would see in the reference:
+  ``obstacles``/``target`` keep their pre-step values (the reference only
+  rebinds them, environment.py:80-81), a held ``states`` receives the moved
+  states and not the re-init (the reference moves in place, :113-123, then
+  rebinds at the re-init, :79).
 * The episode counters live on the device; reading one synchronises.
 * ``env.step`` is the native host engine (``abi.load_host()``, C++): it
   checks the actions, picks the output tensors and enqueues the kernel
@@ -261,21 +261,61 @@ class Env(object):
         fast = (not self._params_dirty and self._rng == 'native'
                 and self._init_sampler is self._default_init_sampler)
         eng.configure(bytes(self._dims), bytes(self._cparams), bytes(b), fast)
-        eng.track_state(self._obstacles, self._target)
+        eng.track_state(self._states, self._obstacles, self._target)
 
     def _unshare_state(self):
-        """Copy-on-write of `obstacles` / `target`: the reference's re-init
-        rebinds them to new tensors (environment.py:79-81) and never writes
-        them in place, so a caller still holding the tensor from before a step
-        keeps its values. The kernel re-initialises finished envs in place;
-        when the engine reports a tensor referenced outside the Env, the Env
-        moves to a copy (stream-ordered) before the step writes."""
-        ob_shared, tg_shared = self._engine.shared_state()
+        """Copy-on-write of the state tensors. The reference's re-init
+        rebinds `states`, `obstacles` and `target` to new tensors
+        (environment.py:79-81), so a caller still holding one from before a
+        step keeps its values - for `states` the moved ones, since
+        `_move_agents` writes it in place first (:113-123). The kernel writes
+        all three in place; when the engine reports one referenced outside
+        the Env, the Env moves to a copy (stream-ordered) before the step.
+        Returns the held pre-step `states` tensor (for `_move_held`) or None."""
+        st_shared, ob_shared, tg_shared = self._engine.shared_state()
+        held = None
+        if st_shared:
+            held = self._states
+            object.__setattr__(self, '_states', held.clone())
         if ob_shared:
             object.__setattr__(self, '_obstacles', self._obstacles.clone())
         if tg_shared:
             object.__setattr__(self, '_target', self._target.clone())
         self._configure()
+        return held
+
+    def _move_held(self, held, actions_ptr):
+        """The reference's in-place `_move_agents` (environment.py:113-123) on
+        a held pre-step `states` tensor: the same step kernel on that tensor
+        with scratch outputs, no truncation and no collisions (trunc_after and
+        the collision distances at +-inf, a zeroed `_terminates`), so no env
+        finishes and the tensor receives exactly the moved states."""
+        P, A = self.num_parallel, self.num_agents
+        dev = self.device
+        out = torch.empty(P * A * self._obs_dim + P, device=dev)
+        flags = torch.zeros(3, P, dtype=torch.uint8, device=dev)
+        step_num = torch.zeros(P, device=dev)
+        b = abi.MarlnavStepBuffers()
+        b.states = held.data_ptr()
+        b.obstacles = self._obstacles.data_ptr()
+        b.target = self._target.data_ptr()
+        b.step_num = step_num.data_ptr()
+        b.terminates = flags[2].data_ptr()
+        b.actions = actions_ptr
+        b.obs = out.data_ptr()
+        b.reward = out[P * A * self._obs_dim:].data_ptr()
+        b.terminated = flags[0].data_ptr()
+        b.truncated = flags[1].data_ptr()
+        # re-init sources the kernel never reads here (no env finishes)
+        b.fresh_states, b.fresh_obstacles, b.fresh_target = b.states, b.obstacles, b.target
+        p = abi.MarlnavParams.from_buffer_copy(self._cparams)
+        p.trunc_after = float('inf')
+        p.ob_coll_dist = p.ag_coll_dist = float('-inf')
+        p.flags &= ~(abi.WRITE_OBS_NORM | abi.FRESH_STATES_FROM_MOVED)
+        abi.check(self._lib.marlnav_step(
+            ctypes.byref(self._dims), ctypes.byref(p), ctypes.byref(b),
+            self._engine.step_idx, _stream_handle(dev)), self._lib)
+        del out, flags, step_num   # stream-ordered: reused after the kernel
 
     def _slots(self):
         n = self._lib.marlnav_counter_slots(ctypes.byref(self._dims))
@@ -552,8 +592,7 @@ class Env(object):
         modes (the host init sampler is called every step, environment.py:78)."""
         if self._params_dirty:
             self._sync_params()
-        if any(self._engine.shared_state()):
-            self._unshare_state()
+        held = self._unshare_state() if any(self._engine.shared_state()) else None
         dev = self.device
         if not (type(actions) is torch.Tensor and actions.dtype is _F32
                 and actions.device == dev and actions.shape == self._act_shape
@@ -564,7 +603,10 @@ class Env(object):
         if self._rng == 'native' and self._init_sampler is self._default_init_sampler:
             if not eng.fast_ok:
                 self._configure()
-            return eng.launch(actions.data_ptr(), None, 0)
+            out = eng.launch(actions.data_ptr(), None, 0)
+            if held is not None:
+                self._move_held(held, actions.data_ptr())
+            return out
         P = self.num_parallel
         fs, fo, ft = self._init_sampler()                # environment.py:78
         S = self._obstacles.shape[1]
@@ -587,6 +629,8 @@ class Env(object):
             if isinstance(init, MockInitializer):
                 init.states = self._states.clone()
         del keep   # stream-ordered: the caching allocator reuses them after the kernel
+        if held is not None:
+            self._move_held(held, actions.data_ptr())
         return out
 
 

@@ -352,27 +352,44 @@ def test_step_outputs_never_alias_live_tensors(pkg):
     assert len(ptrs) <= 4
 
 
-def test_held_obstacles_and_target_are_copied_on_write(pkg):
+def test_held_state_tensors_see_what_the_reference_shows(pkg):
     """The reference never writes obstacles / target in place (its re-init
     rebinds them, environment.py:79-81): a caller holding the pre-step tensor,
-    or a view of it, keeps its values here too. Nothing held: the step writes
-    the Env's buffers in place (no copies). Holders change nothing else: the
-    trajectory equals one run without holders, bit for bit."""
+    or a view of it, keeps its values here too. A held `states` receives the
+    moved states (the reference moves in place, :113-123) but not the re-init
+    (:79 rebinds). Nothing held: the step writes the Env's buffers in place (no
+    copies). Holders change nothing else: the trajectory equals one run
+    without holders, bit for bit."""
     P = 4096 + 7
     env = make_env(pkg, P, 3, 3, episode_len=3)   # every env truncates at step 3
     twin = make_env(pkg, P, 3, 3, episode_len=3)
     acts = [torch.rand(P, 3, 2, device=DEV) - 0.5 for _ in range(3)]
-    p_ob, p_tg = env.obstacles.data_ptr(), env.target.data_ptr()
+    p_st, p_ob, p_tg = env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()
     for k in range(4):
         env.step(acts[k % 3])
         twin.step(acts[k % 3])
-    assert (env.obstacles.data_ptr(), env.target.data_ptr()) == (p_ob, p_tg)
+    assert (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()) == \
+        (p_st, p_ob, p_tg)
     ob, tg_view = env.obstacles, env.target[:, 0]
     ob0, tg0 = ob.clone(), tg_view.clone()
     for k in range(4, 8):
+        if k == 5:   # step 6: every env truncates
+            held, held0 = env.states, env.states.clone()
+            ob_k, tg_k = env.obstacles.clone(), env.target.clone()
         o1 = env.step(acts[k % 3])[0]
         o2 = twin.step(acts[k % 3])[0]
         assert torch.equal(o1._packed, o2._packed)
+        if k == 5:
+            # the moved states alone: the same pre-step state through an Env
+            # in which nothing finishes
+            mv = make_env(pkg, P, 3, 3, episode_len=10 ** 9)
+            mv._ob_coll_dist = mv._ag_coll_dist = float("-inf")
+            mv.states, mv.obstacles, mv.target = held0, ob_k, tg_k
+            mv.step(acts[k % 3])
+            torch.cuda.synchronize()
+            assert torch.equal(held, mv.states)
+            assert not torch.equal(held, env.states)   # the env's own: re-initialised
+            del held, mv
     torch.cuda.synchronize()
     assert torch.equal(ob, ob0) and torch.equal(tg_view, tg0)
     assert env.obstacles.data_ptr() != p_ob and env.target.data_ptr() != p_tg
@@ -382,10 +399,10 @@ def test_held_obstacles_and_target_are_copied_on_write(pkg):
         assert torch.equal(a, b)
     # holders gone (the loop's names too): back to in-place steps
     del ob, tg_view, a, b
-    q_ob, q_tg = env.obstacles.data_ptr(), env.target.data_ptr()
+    q = (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr())
     for k in range(3):
         env.step(acts[k])
-    assert (env.obstacles.data_ptr(), env.target.data_ptr()) == (q_ob, q_tg)
+    assert (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()) == q
 
 
 def test_discounted_returns_match_reference_and_oracle(pkg):
