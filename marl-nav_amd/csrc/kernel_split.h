@@ -206,9 +206,10 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     constexpr int TQ = LPR - 1;  // the lane whose last other-agent / obstacle slot is spare
     const float cap = pr.cap_distance;
     SplitTerms t{0u, 0, 0.0f, 0.0f};
-    // obstacle flags from the nearest obstacle (d < r for some d <=> min d <
-    // r; v_min ignores a NaN distance, which compares false either way)
-    float ob_min = __builtin_inff();
+    // obstacle and other-agent flags from the nearest one (d < r for some d
+    // <=> min d < r; v_min ignores a NaN distance, which compares false
+    // either way)
+    float ob_min = __builtin_inff(), ag_min = __builtin_inff();
     // TFAST (FAST tiles, parameters inside the short sequences' guards,
     // kTermsFastFlag): the bond terms' divisions by the exact short sequences
     static_assert(!TFAST || FAST, "short divisions need the fast coordinate range");
@@ -266,7 +267,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
                 orow[2 + 2 * O + kx] = ang;
                 orow[2 + 2 * O + (A - 1) + kx] = d;
                 if (TERMS) {
-                    t.fl |= (d < pr.ag_risk_dist ? 4u : 0u) | (d < pr.ag_coll_dist ? 8u : 0u);
+                    ag_min = __builtin_fminf(ag_min, d);  // flags after the loop, as for obstacles
                     t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
                     if constexpr (TFAST) {
                         const float sd = div_c(d - pr.ideal_dist, d_sharp, ok);
@@ -279,7 +280,9 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
             }
         }
     }
-    if (TERMS) t.fl |= (ob_min < pr.ob_risk_dist ? 1u : 0u) | (ob_min < pr.ob_coll_dist ? 2u : 0u);
+    if (TERMS)
+        t.fl |= (ob_min < pr.ob_risk_dist ? 1u : 0u) | (ob_min < pr.ob_coll_dist ? 2u : 0u) |
+                (ag_min < pr.ag_risk_dist ? 4u : 0u) | (ag_min < pr.ag_coll_dist ? 8u : 0u);
     return t;
 }
 
