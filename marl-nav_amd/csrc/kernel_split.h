@@ -193,7 +193,7 @@ constexpr bool kSplitTgtInOb = !kSplitTgtInAg<A, O, LPR> && O % LPR != 0;
 
 // unroll factor of split_pairs' obstacle / other-agent loops (timing builds)
 
-template <int A, int O, int LPR, bool TERMS, bool FAST, bool TFAST = false>
+template <int A, int O, int LPR, bool TERMS, bool FAST, bool TFAST = false, bool SHARP1 = false>
 __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
                                                   const float *__restrict__ obe,
                                                   const float *__restrict__ tge, int a, int q,
@@ -214,7 +214,9 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     // kTermsFastFlag): the bond terms' divisions by the exact short sequences
     static_assert(!TFAST || FAST, "short divisions need the fast coordinate range");
     DivC d_sharp{1.0f, 1.0f};
-    if constexpr (TERMS && TFAST) d_sharp = make_divc(pr.bond_sharpness, ok);
+    // SHARP1: bond_sharpness == 1 (the reference's constant, environment.py:
+    // 66), where (d - ideal) / 1 is d - ideal exactly
+    if constexpr (TERMS && TFAST && !SHARP1) d_sharp = make_divc(pr.bond_sharpness, ok);
     if constexpr (!kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>) {
         const float d = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
         const float ang = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, d, cap, ok);
@@ -270,7 +272,8 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
                     ag_min = __builtin_fminf(ag_min, d);  // flags after the loop, as for obstacles
                     t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
                     if constexpr (TFAST) {
-                        const float sd = div_c(d - pr.ideal_dist, d_sharp, ok);
+                        const float sd = SHARP1 ? d - pr.ideal_dist
+                                                : div_c(d - pr.ideal_dist, d_sharp, ok);
                         bond_row[kx] = recip_fast(1.0f + sd * sd, ok);
                     } else {
                         const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
@@ -442,7 +445,11 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         }
         bool unused = true;
         SplitTerms t;
-        if (__builtin_expect(fast, 1) && !OBS_ONLY && (pr.flags & kTermsFastFlag))
+        if (__builtin_expect(fast, 1) && !OBS_ONLY && (pr.flags & kTermsFastFlag) &&
+            pr.bond_sharpness == 1.0f)
+            t = split_pairs<A, O, LPR, !OBS_ONLY, true, true, true>(sts, obe, tge, a, q, ox, oy, dx,
+                                                                   dy, orow, brow, pr, unused);
+        else if (__builtin_expect(fast, 1) && !OBS_ONLY && (pr.flags & kTermsFastFlag))
             t = split_pairs<A, O, LPR, !OBS_ONLY, true, true>(sts, obe, tge, a, q, ox, oy, dx, dy,
                                                              orow, brow, pr, unused);
         else if (__builtin_expect(fast, 1))
