@@ -103,6 +103,38 @@ def test_engine_fast_path_falls_back_for_other_actions():
     assert calls == []
 
 
+def test_engine_reports_held_state_tensors():
+    """Copy-on-write rule for states / obstacles / target (environment.py:
+    79-81 rebind them): a tracked tensor counts as held once
+    anything beyond its owner's attribute and the engine refers to it, or a
+    view shares its storage; a held tensor keeps steps off the fast path."""
+    calls = []
+    eng, cb = _cpu_engine(calls)
+
+    class Owner:
+        pass
+    o = Owner()
+    o.s, o.ob, o.tg = torch.zeros(10, 3, 5), torch.zeros(10, 3, 2), torch.zeros(10, 1, 2)
+    eng.track_state(o.s, o.ob, o.tg)
+    assert eng.shared_state() == (False, False, False)
+    s = o.s
+    assert eng.shared_state() == (True, False, False)
+    del s
+    v = o.tg[:, 0]
+    assert eng.shared_state() == (False, False, True)
+    del v
+    lst = [o.ob]
+    assert eng.shared_state() == (False, True, False)
+    del lst
+    assert eng.shared_state() == (False, False, False)
+    # re-tracking releases the old tensors
+    old = o.s
+    o.s = o.s.clone()
+    eng.track_state(o.s, o.ob, o.tg)
+    assert eng.shared_state() == (False, False, False)
+    del old
+
+
 def test_cli_mirrors_reference_arguments():
     """python -m marlnav_amd takes the reference's arguments with its
     defaults (marlnav/__main__.py:49-132; utils.default_args restates them)."""
