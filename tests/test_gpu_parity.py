@@ -405,6 +405,25 @@ def test_held_state_tensors_see_what_the_reference_shows(pkg):
     assert (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()) == q
 
 
+def test_held_states_reference_rng_mode(pkg):
+    """The same held-`states` rule through Env._step_py's reference-RNG
+    branch (host-drawn fresh candidates every step, environment.py:78)."""
+    P = 3000 + 5
+    env = make_env(pkg, P, 3, 3, episode_len=2, rng="reference")
+    acts = torch.rand(P, 3, 2, device=DEV) - 0.5
+    env.step(acts)
+    held, held0 = env.states, env.states.clone()
+    ob_k, tg_k = env.obstacles.clone(), env.target.clone()
+    env.step(acts)                      # step 2: every env truncates
+    mv = make_env(pkg, P, 3, 3, episode_len=10 ** 9)
+    mv._ob_coll_dist = mv._ag_coll_dist = float("-inf")
+    mv.states, mv.obstacles, mv.target = held0, ob_k, tg_k
+    mv.step(acts)
+    torch.cuda.synchronize()
+    assert torch.equal(held, mv.states)
+    assert not torch.equal(held, env.states)
+
+
 def test_discounted_returns_match_reference_and_oracle(pkg):
     """§8(f) row 3: the device scan against MAPPO._process_rewards run
     unmodified (F5) and the C oracle at rollout size; float64 within 1e-12."""
