@@ -14,8 +14,13 @@ independent slice of global env ids [rank*P, (rank+1)*P) (weak scaling); the
 data path has no collective. A step = one ``Env.step`` call, through the
 Python API, returning fresh observation/reward/done tensors.
 
-Timing: W untimed steps; barrier + synchronize; K timed steps; synchronize +
-barrier; the max over ranks. value = N*P*K / max time.
+Timing: a GPU clock ramp (``--prewarm`` seconds of back-to-back steps of a
+second, scratch Env of the same shape, before anything of the timed Env
+runs: an idle MI355X starts the first milliseconds of a process at low
+clocks, which at the driver's 20-step setting was the difference between
+9 and 22 us per step on the same box); W untimed steps of the timed Env;
+barrier + synchronize; K timed steps; synchronize + barrier; the max over
+ranks. value = N*P*K / max time.
 
 roofline (the step kernel): ``kernel_us`` = average duration of one step
 launch, from HIP events on the launch stream around replays of a hipGraph of
@@ -65,6 +70,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", type=int, choices=(0, 1, 2, 3, 4), default=None,
+                    help="a BASELINE.json configs[i] shape (overrides --envs/--agents/"
+                         "--obstacles); 4 = 131072 envs split over the --gpus ranks")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--agents", type=int, default=3)
     ap.add_argument("--obstacles", type=int, default=3)
@@ -72,7 +80,36 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="seconds of CPU-baseline work per thread setting")
     ap.add_argument("--pmc", default=PMC_SUMMARY)
+    ap.add_argument("--prewarm", type=float, default=0.3,
+                    help="seconds of scratch-Env steps before the timed Env starts")
     return ap.parse_args(argv)
+
+
+# BASELINE.json configs: (envs, agents, obstacles); configs[4]'s envs are the
+# global count, split over the ranks (strong scaling)
+BASELINE_CONFIGS = {0: (2, 3, 3), 1: (1024, 3, 8), 2: (65536, 3, 3), 3: (4096, 16, 32),
+                    4: (131072, 3, 3)}
+
+
+def workload(a, world):
+    """(envs per GPU, A, O, label, scaling) of this run."""
+    if a.config is not None:
+        P, A, O = BASELINE_CONFIGS[a.config]
+        if a.config == 4:
+            if P % world:
+                raise SystemExit(f"configs[4]: 131072 envs do not split over {world} ranks")
+            return (P // world, A, O,
+                    f"BASELINE configs[4]: 131072 envs x 3 agents x 3 obstacles over {world} "
+                    f"GPU(s), {P // world} per GPU", "strong")
+        return P, A, O, f"BASELINE configs[{a.config}]", "weak"
+    P, A, O = a.envs, a.agents, a.obstacles
+    for i, shape in BASELINE_CONFIGS.items():
+        if (P, A, O) == shape and i != 4:
+            return P, A, O, f"BASELINE configs[{i}]", "weak"
+    if (P * world, A, O) == BASELINE_CONFIGS[4]:
+        return P, A, O, (f"BASELINE configs[4]: 131072 envs x 3 agents x 3 obstacles over "
+                         f"{world} GPU(s), {P} per GPU"), "weak"
+    return P, A, O, "custom", "weak"
 
 
 def self_launch(a):
@@ -137,6 +174,19 @@ def kernel_time_us(env, actions, n=25, replays=12):
         per.append(s.elapsed_time(e) * 1e3 / n)
     per.sort()
     return sum(per) / len(per), per[len(per) // 2]
+
+
+def prewarm(env, actions, seconds):
+    """Back-to-back steps of a scratch Env for ``seconds`` (GPU clock ramp;
+    nothing of the timed Env runs here). Returns the steps taken."""
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(64):
+            env.step(actions[n % len(actions)])
+            n += 1
+        torch.cuda.synchronize()
+    return n
 
 
 def host_cpu_facts():
@@ -253,9 +303,11 @@ def main():
     red_dev = device if backend == "nccl" else None
 
     import marlnav_amd as pkg
-    P, A, O = a.envs, a.agents, a.obstacles
+    P, A, O, cfg_name, scaling = workload(a, world)
     env = make_env(pkg, P, A, O, device, rank)
     actions = make_actions(P, A, device, rank)
+    kenv = make_env(pkg, P, A, O, device, rank, seed=20251004)
+    prewarm_steps = prewarm(kenv, actions, a.prewarm)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record()   # the first timing event of a process is slow to record:
@@ -296,7 +348,6 @@ def main():
     torch.cuda.synchronize()
     region_us = ev0.elapsed_time(ev1) * 1e3 / a.steps
 
-    kenv = make_env(pkg, P, A, O, device, rank, seed=20251004)
     kern_us, kern_med = kernel_time_us(kenv, actions)
     del kenv
     per_env = alg_bytes_per_env(A, O)
@@ -310,7 +361,6 @@ def main():
         cpu = cpu_baseline(P, A, O, a.cpu_seconds, device)
 
     if rank == 0:
-        cfg_name = "BASELINE configs[2]" if (P, A, O) == (65536, 3, 3) else "custom"
         line = {
             "metric": "env-steps/sec (whole node) at 3 agents; 1/2/4/8-GPU scaling + %HBM roofline",
             "value": world * P * a.steps / dt,
@@ -320,12 +370,13 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": dt * 1e3 / a.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: native triangle init, U(-0.5,0.5) angle/accel actions",
             "config": {"workload": f"{P} envs x {A} agents x {O} obstacles per GPU "
                                    f"({cfg_name}); Env.step via C ABI",
+                       "baseline_config": cfg_name,
                        "envs_per_gpu": P, "agents": A, "obstacles": O,
                        "global_envs": world * P, "episode_len": 200,
                        "parallelism": f"independent env slices x{world}, no collective"},
@@ -337,6 +388,7 @@ def main():
                          "alg_bytes_per_launch": launch_bytes,
                          "alg_bytes_per_env_step": per_env},
             "cpu_baseline": cpu,
+            "prewarm": {"seconds": a.prewarm, "scratch_env_steps": prewarm_steps},
             "episode_counters": counters,
         }
         print(json.dumps(line), flush=True)

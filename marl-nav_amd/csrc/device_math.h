@@ -250,30 +250,43 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
     return dist < cap ? 0.0f : ang;
 }
 
-// sin/cos of an angle already clamped to [-pi, pi] in fp32 (<= 1 ulp, like
-// torch's SLEEF sin/cos on the reference's CPU path): three-part Cody-Waite
-// reduction by pi/2 (|k| <= 2, every product exact), the Cephes single-
-// precision minimax polynomials on [-pi/4, pi/4] (cosine with the 1 - z/2
-// rounding error carried), quadrant by comparisons (NaN -> quadrant 0, so
-// NaN propagates). The identical operation sequence is oracle_sincos in
-// oracle/marlnav_oracle.c (both built without FMA contraction), so kernel
-// and oracle agree bit for bit.
+// Correctly rounded fp32 sin/cos of an angle already clamped to [-pi, pi]
+// (the heading update, environment.py:131-137). The reference evaluates
+// torch.sin/cos on its CPU path, which in this torch build is MKL VML
+// (vsSin/vsCos, <= 0.6 ulp, not correctly rounded); no fp32 sequence of ours
+// can reproduce MKL's, and the correctly rounded value is the one that
+// agrees with it most often (tests/golden/libm_check.py sweeps every fp32
+// angle in [-pi, pi]: CR agrees with MKL on 95.1% of sines and cosines, the
+// round-2 fp32 Cephes polynomials on 87-89%). Evaluated in fp64: two-part
+// Cody-Waite reduction by pi/2 (|k| <= 2; k*PIO2_1 and x - k*PIO2_1 exact),
+// the fdlibm __kernel_sin / __kernel_cos minimax polynomials on [-pi/4, pi/4]
+// (error < 2^-58), one rounding to fp32 at the end. The sweep checks the
+// result against a correctly rounded reference for every input of the range.
+// NaN -> quadrant 0 (NaN propagates); sin(-0) = -0. The identical operation
+// sequence (explicit FMAs, no contraction) is oracle_sincos in
+// oracle/marlnav_oracle.c, so kernel and oracle agree bit for bit.
 __device__ __forceinline__ void sincos_k(float th, float *s_out, float *c_out)
 {
-    const float k = __builtin_rintf(th * 0.636619772f);
-    float r = __builtin_fmaf(-k, 1.5703125f, th);
-    r = __builtin_fmaf(-k, 4.837512969970703125e-4f, r);
-    r = __builtin_fmaf(-k, 7.54978995489188216e-8f, r);
-    r = k == 0.0f ? th : r;  // keeps the sign of -0
-    const float z = r * r;
-    float ps = __builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f);
-    ps = __builtin_fmaf(ps, z, -1.6666654611e-1f);
-    const float sn = r == 0.0f ? r : __builtin_fmaf(r * z, ps, r);  // sin(-0) = -0
-    float pc = __builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f);
-    pc = __builtin_fmaf(pc, z, 4.166664568298827e-2f);
-    const float hz = 0.5f * z, w = 1.0f - hz;
-    const float cs = w + (((1.0f - w) - hz) + (z * z) * pc);
-    const bool q1 = k == 1.0f, q3 = k == -1.0f, q2 = k == 2.0f || k == -2.0f;
+    const double x = (double)th;
+    const double k = __builtin_rint(x * 6.36619772367581382433e-01);
+    double r = __builtin_fma(-k, 1.57079632673412561417e+00, x);
+    r = __builtin_fma(-k, 6.07710050650619224932e-11, r);
+    r = k == 0.0 ? x : r;  // keeps the sign of -0
+    const double z = r * r;
+    double ps = __builtin_fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+    ps = __builtin_fma(z, ps, 2.75573137070700676789e-06);
+    ps = __builtin_fma(z, ps, -1.98412698298579493134e-04);
+    ps = __builtin_fma(z, ps, 8.33333333332248946124e-03);
+    ps = __builtin_fma(z, ps, -1.66666666666666324348e-01);
+    const double sd = r == 0.0 ? r : __builtin_fma(z * r, ps, r);  // sin(-0) = -0
+    double pc = __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+    pc = __builtin_fma(z, pc, -2.75573143513906633035e-07);
+    pc = __builtin_fma(z, pc, 2.48015872894767294178e-05);
+    pc = __builtin_fma(z, pc, -1.38888888888741095749e-03);
+    pc = __builtin_fma(z, pc, 4.16666666666666019037e-02);
+    const double cd = __builtin_fma(z * z, pc, __builtin_fma(-0.5, z, 1.0));
+    const float sn = (float)sd, cs = (float)cd;
+    const bool q1 = k == 1.0, q3 = k == -1.0, q2 = k == 2.0 || k == -2.0;
     *s_out = q1 ? cs : (q3 ? -cs : (q2 ? -sn : sn));
     *c_out = q1 ? -sn : (q3 ? sn : (q2 ? -cs : cs));
 }

@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(64 * A)
                       reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
             }
             const uint64_t fm = __ballot(fin);
-            if (fm) {
+            if (fm && !(MARLNAV_AB & 1)) {
                 int *wlist = reinterpret_cast<int *>(lds + BP::LIST2) + E * (w - 1);
                 if (fin)
                     wlist[__builtin_amdgcn_mbcnt_hi(
@@ -387,6 +387,7 @@ __global__ void __launch_bounds__(64 * A)
     }
     STAMP(5);
     if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
+        if (!(MARLNAV_AB & 2))
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
                                                st, tid);  // (E = 64: whole 16-byte pieces)
     } else if (!OBS_ONLY && full && NT % D == 0) {

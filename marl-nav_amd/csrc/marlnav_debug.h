@@ -24,3 +24,9 @@ __device__ unsigned long long *g_stamps;
     do {         \
     } while (0)
 #endif
+
+// Timing-only ablation switches of A/B variant builds (scripts/build_variant.sh
+// ... -DMARLNAV_AB=bits); 0 in the product build.
+#ifndef MARLNAV_AB
+#define MARLNAV_AB 0
+#endif

@@ -26,10 +26,11 @@
 // Numerics: built with -ffp-contract=off and the HIP default
 // correctly rounded fp32 division and sqrt, so every distance, dot product
 // and reward term is the fp32 expression the reference's CPU path evaluates,
-// summed in torch's order. sin/cos of the heading update are fp32 (<= 1 ulp:
-// Cody-Waite reduction and the Cephes polynomials, sincos_k, the same
-// operation sequence as oracle_sincos in oracle/marlnav_oracle.c); acos is
-// the device libm's acosf.
+// summed in torch's order. sin/cos of the heading update are correctly
+// rounded (fp64 evaluation rounded once, sincos_k, the same operation
+// sequence as oracle_sincos in oracle/marlnav_oracle.c; the reference's MKL
+// VML sin/cos agrees with it on 95% of angles); acos is the device libm's
+// acosf.
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>

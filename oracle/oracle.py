@@ -46,6 +46,16 @@ def load():
         lib.oracle_normalize.restype = None
         lib.oracle_sincos.argtypes = [ctypes.c_float, P, P]
         lib.oracle_sincos.restype = None
+        lib.oracle_sincos_range.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int, P, P]
+        lib.oracle_sincos_range.restype = None
+        lib.oracle_acosf_range.argtypes = [ctypes.c_uint32, ctypes.c_int64, P]
+        lib.oracle_acosf_range.restype = None
+        lib.oracle_set_heading_sincos.argtypes = [P, P]
+        lib.oracle_set_heading_sincos.restype = None
+        lib.oracle_sincos_n.argtypes = [ctypes.c_int64, P, ctypes.c_int, P, P]
+        lib.oracle_sincos_n.restype = None
+        lib.oracle_acosf_n.argtypes = [ctypes.c_int64, P, P]
+        lib.oracle_acosf_n.restype = None
         lib.oracle_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P,
                                                   ctypes.c_double, P, P]
         lib.oracle_discounted_returns.restype = None
@@ -92,10 +102,12 @@ def observe(dims, states, obstacles, target, params=None):
 
 
 def step(dims, params, states, obstacles, target, step_num, terminates, actions,
-         fresh=None, formation=None, step_idx=0, norm=None):
+         fresh=None, formation=None, step_idx=0, norm=None, heading_sincos=None):
     """One Env.step on copies of the inputs. Returns a dict of outputs:
     states, obstacles, target, step_num, terminates, obs (P,A,D), reward,
-    terminated, truncated, counters (trunc, col, tar), obs_norm (if norm)."""
+    terminated, truncated, counters (trunc, col, tar), obs_norm (if norm).
+    ``heading_sincos``: (sin, cos) per (env, agent) to use in the move instead
+    of oracle_sincos (a test injecting the reference's own torch.sin/cos)."""
     P, A, O = dims.num_parallel, dims.num_agents, dims.num_obstacles
     D = obs_dim(A, O)
     out = {
@@ -126,8 +138,18 @@ def step(dims, params, states, obstacles, target, step_num, terminates, actions,
         out["obs_norm"] = np.empty((P, A, D), np.float32)
         keep += [mean, scale]
         b.obs_norm, b.norm_mean, b.norm_scale = _ptr(out["obs_norm"]), _ptr(mean), _ptr(scale)
-    load().oracle_step(ctypes.byref(dims), ctypes.byref(params), ctypes.byref(b),
-                       int(step_idx), 1)
+    lib = load()
+    if heading_sincos is not None:
+        hs, hc = (_f32(x).reshape(-1) for x in heading_sincos)
+        assert hs.size == P * A and hc.size == P * A
+        keep += [hs, hc]
+        lib.oracle_set_heading_sincos(_ptr(hs), _ptr(hc))
+    try:
+        lib.oracle_step(ctypes.byref(dims), ctypes.byref(params), ctypes.byref(b),
+                        int(step_idx), 1)
+    finally:
+        if heading_sincos is not None:
+            lib.oracle_set_heading_sincos(None, None)
     out["counters"] = out["counters"].astype(np.int64)
     return out
 
@@ -151,17 +173,39 @@ def philox(ctr, key):
     return o
 
 
-def sincos(th):
-    """oracle_sincos over an array: (sin, cos) as float32 arrays."""
+def sincos(th, which=0):
+    """oracle_sincos over an array: (sin, cos) as float32 arrays (which=1:
+    the round-2 fp32 Cephes sequence, for tests/golden/libm_check.py)."""
     th = np.ascontiguousarray(th, np.float32).ravel()
     s = np.empty_like(th)
     c = np.empty_like(th)
-    lib = load()
-    sp, cp = ctypes.c_float(), ctypes.c_float()
-    for i, v in enumerate(th):
-        lib.oracle_sincos(float(v), ctypes.byref(sp), ctypes.byref(cp))
-        s[i], c[i] = sp.value, cp.value
+    load().oracle_sincos_n(th.size, _ptr(th), int(which), _ptr(s), _ptr(c))
     return s, c
+
+
+def acosf(x):
+    """The oracle's acos (libm acosf) over an array."""
+    x = np.ascontiguousarray(x, np.float32).ravel()
+    out = np.empty_like(x)
+    load().oracle_acosf_n(x.size, _ptr(x), _ptr(out))
+    return out
+
+
+def sincos_range(first_bits, n, which=0):
+    """sin/cos of the n consecutive fp32 bit patterns from ``first_bits``:
+    which=0 oracle_sincos (the step's), 1 the round-2 fp32 Cephes sequence
+    (tests/golden/libm_check.py). The C loop runs without the GIL."""
+    s = np.empty(n, np.float32)
+    c = np.empty(n, np.float32)
+    load().oracle_sincos_range(int(first_bits), int(n), int(which), _ptr(s), _ptr(c))
+    return s, c
+
+
+def acosf_range(first_bits, n):
+    """libm acosf (the oracle's) of n consecutive fp32 bit patterns."""
+    out = np.empty(n, np.float32)
+    load().oracle_acosf_range(int(first_bits), int(n), _ptr(out))
+    return out
 
 
 def split_obs(obs, A, O):
