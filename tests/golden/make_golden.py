@@ -383,9 +383,14 @@ def main():
                 "cpu_capability": torch.backends.cpu.get_cpu_capability(),
                 "reference": "JussiM01/MARL-nav @ 2025-10-03 (imported unmodified)",
                 "generator": "tests/golden/make_golden.py", "files": {}}
-    if cli.only and os.path.exists(mpath):
+    if os.path.exists(mpath):
         with open(mpath) as fh:
-            manifest["files"] = json.load(fh)["files"]
+            old = json.load(fh)
+        # entries other scripts own (tests/golden/libm_check.py: "libm")
+        for k, v in old.items():
+            manifest.setdefault(k, v)
+        if cli.only:
+            manifest["files"] = old["files"]
     for name, arrays, meta in jobs:
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **arrays)
