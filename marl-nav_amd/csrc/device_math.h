@@ -42,6 +42,84 @@ __device__ __forceinline__ void out_st4(float *p, float4 v)
         *reinterpret_cast<float4 *>(p) = v;
 }
 
+// ---------------------------------------------------- written-through outputs
+// The env-block kernel's outputs (observation rows, states, per-env scalars)
+// leave through buffer stores with a system-scope cache policy (sc0 sc1):
+// they are written through the XCD's L2 to memory as they are issued, so the
+// end-of-launch L2 write-back - which a plain or `nt` store leaves with every
+// dirty line of the launch (14 MB at 65536x3x3, all written in the last
+// microsecond) - has nothing left to flush. Buffer stores carry the policy
+// as an operand the compiler tracks (an inline-asm global store would hide
+// its vmcnt from the waitcnt insertion), and the resource's byte size bounds
+// every store to its span. Only launches that write at least
+// kWriteThroughMinBytes take this path: below that the end-of-launch
+// write-back is short and waiting for memory acknowledgements at the wave's
+// end is not (A/B on two boxes, graph replay, nt -> written through:
+// 65536x3x3 (14 MB) 8.38 -> 7.84 and 8.52 -> 8.19 us, 4096x16x32 (27 MB)
+// 13.97 -> 13.13 and 13.89 -> 13.68, 512x16x32 (3.3 MB) 9.17 -> 9.66, 8192x3x3
+// (1.8 MB) 5.57 -> 5.73, 16384x3x3 (3.5 MB) 5.82 -> 5.62 and 5.78 -> 5.80).
+// marlnav_step / marlnav_observe set kWriteThroughFlag in
+// MarlnavParams.flags; `wt` in the kernels is that bit.
+#ifndef MARLNAV_CPOL
+#define MARLNAV_CPOL 17  // SC0 | SC1
+#endif
+constexpr int kCpolOut = MARLNAV_CPOL < 0 ? 0 : MARLNAV_CPOL;
+constexpr bool kWtOut = MARLNAV_CPOL >= 0;
+constexpr uint32_t kWriteThroughFlag = 1u << 29;  // internal MarlnavParams.flags bit
+constexpr int64_t kWriteThroughMinBytes = 8 << 20;
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+
+struct OutBuf {
+    __amdgpu_buffer_rsrc_t r;
+};
+
+// a wave-uniform output span of `bytes` bytes at `base` (raw buffer: stores
+// past `bytes` are dropped)
+__device__ __forceinline__ OutBuf out_buf(const void *base, uint32_t bytes)
+{
+    return OutBuf{__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes,
+                                                     0x00020000)};
+}
+
+__device__ __forceinline__ void wt_st(OutBuf b, uint32_t off, float v)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), b.r, (int)off, 0, kCpolOut);
+}
+
+__device__ __forceinline__ void wt_st(OutBuf b, uint32_t off, uint8_t v)
+{
+    __builtin_amdgcn_raw_buffer_store_b8((char)v, b.r, (int)off, 0, kCpolOut);
+}
+
+__device__ __forceinline__ void wt_st2(OutBuf b, uint32_t off, float2 v)
+{
+    const v2i_t x{__float_as_int(v.x), __float_as_int(v.y)};
+    __builtin_amdgcn_raw_buffer_store_b64(x, b.r, (int)off, 0, kCpolOut);
+}
+
+__device__ __forceinline__ void wt_st4(OutBuf b, uint32_t off, float4 v)
+{
+    const v4i_t x{__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z),
+                  __float_as_int(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(x, b.r, (int)off, 0, kCpolOut);
+}
+
+// Element idx of a global output array, written through (kWtOut; the buffer
+// base is the first active lane's element, so any idx works) or plain.
+template <class T>
+__device__ __forceinline__ void out_el(T *arr, int64_t idx, T v, bool wt)
+{
+    if (kWtOut && wt) {
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)idx);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)idx >> 32));
+        const int64_t ib = (int64_t)(((uint64_t)hi << 32) | lo);
+        wt_st(out_buf(arr + ib, 1u << 26), (uint32_t)(idx - ib) * (uint32_t)sizeof(T), v);
+    } else {
+        out_st(arr + idx, v);
+    }
+}
+
 template <bool NT = kNtOther>
 __device__ __forceinline__ void out_st2(float *p, float2 v)
 {
@@ -528,20 +606,37 @@ __device__ __forceinline__ void stage_spans(Span a, Span b, Span c, int lane)
 __device__ __forceinline__ void wave_store(float *__restrict__ dst, const float *__restrict__ src,
                                            int n, int lane, float *__restrict__ nrm_dst,
                                            const float *__restrict__ mean,
-                                           const float *__restrict__ scale, int D)
+                                           const float *__restrict__ scale, int D, bool wt)
 {
     int head = 0;
+    const OutBuf ob = out_buf(dst, 4u * n);
+    wt = kWtOut && wt;
     if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
         const int n4 = n >> 2;
-        for (int i = lane; i < n4; i += 64)
-            out_st4(dst + 4 * i, *reinterpret_cast<const float4 *>(src + 4 * i));
+        for (int i = lane; i < n4; i += 64) {
+            const float4 v = *reinterpret_cast<const float4 *>(src + 4 * i);
+            if (wt)
+                wt_st4(ob, 16u * i, v);
+            else
+                out_st4(dst + 4 * i, v);
+        }
         head = n4 << 2;
     }
-    for (int i = head + lane; i < n; i += 64) out_st(dst + i, src[i]);
+    for (int i = head + lane; i < n; i += 64) {
+        if (wt)
+            wt_st(ob, 4u * i, src[i]);
+        else
+            out_st(dst + i, src[i]);
+    }
     if (nrm_dst) {
+        const OutBuf nb = out_buf(nrm_dst, 4u * n);
         for (int i = lane; i < n; i += 64) {
             const int k = i % D;
-            nrm_dst[i] = (src[i] - mean[k]) / scale[k];
+            const float v = (src[i] - mean[k]) / scale[k];
+            if (wt)
+                wt_st(nb, 4u * i, v);
+            else
+                nrm_dst[i] = v;
         }
     }
 }
@@ -794,9 +889,28 @@ __device__ __forceinline__ RowOut observe_row_regs(const float *__restrict__ sts
 
 // Store a register row of D floats with the widest aligned vector stores.
 template <int D>
-__device__ __forceinline__ void store_row(float *__restrict__ dst, const float *row)
+__device__ __forceinline__ void store_row(float *__restrict__ dst, const float *row, bool wt)
 {
-    if constexpr (D % 4 == 0) {
+    if (kWtOut && wt) {
+        // per-lane row pointers: one written-through buffer from the first
+        // active lane's row
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)(uintptr_t)dst >> 32));
+        float *b0 = reinterpret_cast<float *>(((uint64_t)hi << 32) | lo);
+        const OutBuf ob = out_buf(b0, 1u << 26);
+        const uint32_t off = (uint32_t)((const char *)dst - (const char *)b0);
+        if constexpr (D % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < D; k += 4)
+                wt_st4(ob, off + 4u * k, make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]));
+        } else if constexpr (D % 2 == 0) {
+#pragma unroll
+            for (int k = 0; k < D; k += 2) wt_st2(ob, off + 4u * k, make_float2(row[k], row[k + 1]));
+        } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) wt_st(ob, off + 4u * k, row[k]);
+        }
+    } else if constexpr (D % 4 == 0) {
 #pragma unroll
         for (int k = 0; k < D; k += 4)
             out_st4(dst + k, make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]));

@@ -58,9 +58,16 @@ __device__ __forceinline__ void block_copy(const T *__restrict__ src, T *__restr
 // LDS span -> global span of n floats by the block's threads; 16-byte
 // vectors for the aligned head (both bases 16-byte aligned by construction)
 __device__ __forceinline__ void block_store(float *__restrict__ dst, const float *__restrict__ src,
-                                            int n, int tid, int nt)
+                                            int n, int tid, int nt, bool wt)
 {
     const int n4 = n >> 2;
+    if (kWtOut && wt) {
+        const OutBuf ob = out_buf(dst, (uint32_t)n * 4u);
+        for (int i = tid; i < n4; i += nt)
+            wt_st4(ob, 16u * i, reinterpret_cast<const float4 *>(src)[i]);
+        for (int i = (n4 << 2) + tid; i < n; i += nt) wt_st(ob, 4u * i, src[i]);
+        return;
+    }
     for (int i = tid; i < n4; i += nt)
         out_st4<kNtRows>(dst + 4 * i, reinterpret_cast<const float4 *>(src)[i]);
     for (int i = (n4 << 2) + tid; i < n; i += nt) out_st<kNtRows>(dst + i, src[i]);
@@ -72,7 +79,7 @@ __device__ __forceinline__ void block_store(float *__restrict__ dst, const float
 template <int N1, int N2, int NT>
 __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float *__restrict__ s1,
                                              float *__restrict__ d2, const float *__restrict__ s2,
-                                             int tid)
+                                             int tid, bool wt)
 {
     static_assert(N1 % 4 == 0 && N2 % 4 == 0, "whole 16-byte pieces");
     constexpr int Q1 = N1 / 4, Q2 = N2 / 4, K1 = (Q1 + NT - 1) / NT, K2 = (Q2 + NT - 1) / NT;
@@ -85,6 +92,16 @@ __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float
     for (int k = 0; k < K2; ++k)
         if ((k + 1) * NT <= Q2 || tid + k * NT < Q2)
             v2[k] = reinterpret_cast<const float4 *>(s2)[tid + k * NT];
+    if (kWtOut && wt) {
+        const OutBuf o1 = out_buf(d1, N1 * 4), o2 = out_buf(d2, N2 * 4);
+#pragma unroll
+        for (int k = 0; k < K1; ++k)
+            if ((k + 1) * NT <= Q1 || tid + k * NT < Q1) wt_st4(o1, 16u * (tid + k * NT), v1[k]);
+#pragma unroll
+        for (int k = 0; k < K2; ++k)
+            if ((k + 1) * NT <= Q2 || tid + k * NT < Q2) wt_st4(o2, 16u * (tid + k * NT), v2[k]);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < K1; ++k)
         if ((k + 1) * NT <= Q1 || tid + k * NT < Q1) out_st4<kNtRows>(d1 + 4 * (tid + k * NT), v1[k]);
@@ -159,6 +176,7 @@ __global__ void __launch_bounds__(64 * A)
         }
     }
     const MarlnavParams pr = load_params(K);
+    const bool wt = (pr.flags & kWriteThroughFlag) != 0;  // written-through outputs
     const int l = (int)lane;  // env of this lane within the block
     const int r = l * A + w;  // row of this lane
     const bool row_on = l < ne;
@@ -257,7 +275,7 @@ __global__ void __launch_bounds__(64 * A)
     __syncthreads();
     STAMP(3);
     float *gobs = in_sgpr(b.obs + e0 * (A * D));
-    if (OBS_ONLY) block_store(gobs, obs_rows, nrow * D, tid, NT);
+    if (OBS_ONLY) block_store(gobs, obs_rows, nrow * D, tid, NT, wt);
     const bool norm = !OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM);
     if (!OBS_ONLY) {
         int *list = reinterpret_cast<int *>(lds + BP::LIST);
@@ -286,15 +304,15 @@ __global__ void __launch_bounds__(64 * A)
 #pragma unroll
                 for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
-                out_st(&b.reward[e], rsum / (float)A);                     // torch.mean (:233)
+                out_el(b.reward, e, rsum / (float)A, wt);              // torch.mean (:233)
 
                 float step_num = lds[BP::SN + l] + 1.0f;           // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
                 const bool terminated = any_col || term_old;       // :213-214
-                out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
-                out_st(&b.terminated[e], (uint8_t)terminated);
-                out_st(&b.truncated[e], (uint8_t)truncated);
+                out_el(b.terminates, e, (uint8_t)(!term_old && all_in), wt);  // :218-219
+                out_el(b.terminated, e, (uint8_t)terminated, wt);
+                out_el(b.truncated, e, (uint8_t)truncated, wt);
                 fin = truncated || terminated;                     // :102-104
                 if (NOISY && fin) {  // noisy native re-init: serial per env
                     KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -315,12 +333,12 @@ __global__ void __launch_bounds__(64 * A)
                                                 (uint64_t)(kl->a.env_offset + e), kl->a.step_idx,
                                                 st + 5 * A * l, obl, tgl);
                         float *gob = kl->a.b.obstacles;
-                        for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
-                        kl->a.b.target[2 * e] = tgl[0];
-                        kl->a.b.target[2 * e + 1] = tgl[1];
+                        for (int i = 0; i < 2 * O; ++i) out_el(gob, e * O * 2 + i, obl[i], wt);
+                        out_el(kl->a.b.target, 2 * e, tgl[0], wt);
+                        out_el(kl->a.b.target, 2 * e + 1, tgl[1], wt);
                     }
                 }
-                out_st(&b.step_num[e], fin ? blend_in(step_num, 0.0f) : step_num);
+                out_el(b.step_num, e, fin ? blend_in(step_num, 0.0f) : step_num, wt);
                 tr_l = truncated;
                 co_l = any_col;
                 ta_l = all_in;
@@ -369,6 +387,9 @@ __global__ void __launch_bounds__(64 * A)
                 wave_sync();  // every lane of this wave sees its list
                 reinit_reobs_native<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, wlist,
                                           (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
+                if (MARLNAV_AB & 8)
+                    reinit_reobs_native<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, wlist,
+                                              (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
             }
         }
         __syncthreads();
@@ -389,14 +410,14 @@ __global__ void __launch_bounds__(64 * A)
     if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
         if (!(MARLNAV_AB & 2))
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
-                                               st, tid);  // (E = 64: whole 16-byte pieces)
+                                               st, tid, wt);  // (E = 64: whole 16-byte pieces)
     } else if (!OBS_ONLY && full && NT % D == 0) {
         // ---- the same with the fused ObsNormalizer (utils.py:519-532):
         // thread tid only ever meets feature tid % D (NT is a multiple of D),
         // so its mean and scale are loaded once; every LDS read and every
         // division is issued ahead of the stores
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
-                                               st, tid);
+                                               st, tid, wt);
         KArgsK *kl = kargs_late<kHotKargsOff>();
         const int kk = tid % D;
         const float m = kl->a.b.norm_mean[kk], sc = kl->a.b.norm_scale[kk];
@@ -409,9 +430,14 @@ __global__ void __launch_bounds__(64 * A)
 #pragma unroll
         for (int k = 0; k < K; ++k) v[k] = (v[k] - m) / sc;
 #pragma unroll
-        for (int k = 0; k < K; ++k) out_st<kNtRows>(gn + tid + k * NT, v[k]);
+        for (int k = 0; k < K; ++k) {
+            if (kWtOut && wt)
+                wt_st(out_buf(gn, E * A * D * 4), 4u * (tid + k * NT), v[k]);
+            else
+                out_st<kNtRows>(gn + tid + k * NT, v[k]);
+        }
     } else if (!OBS_ONLY) {
-        block_store(gobs, obs_rows, nrow * D, tid, NT);
+        block_store(gobs, obs_rows, nrow * D, tid, NT, wt);
         if (norm) {
             // mean and scale staged in LDS once (the reward-term slots are
             // free after the per-env phase), then one pass over the rows
@@ -430,7 +456,7 @@ __global__ void __launch_bounds__(64 * A)
                 gn[i] = (obs_rows[i] - ms[kk]) / ms[D + kk];
             }
         }
-        block_store(in_sgpr(b.states + e0 * (A * 5)), st, nrow * 5, tid, NT);
+        block_store(in_sgpr(b.states + e0 * (A * 5)), st, nrow * 5, tid, NT, wt);
     }
     STAMP(6);
 #if MARLNAV_STAMPS

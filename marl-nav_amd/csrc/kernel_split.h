@@ -353,6 +353,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         term_in = b.terminates[e0 + lane];
     }
     const MarlnavParams pr = load_params(K);
+    const bool wt = (pr.flags & kWriteThroughFlag) != 0;  // written-through outputs
     const int row = (int)lane / LPR, q = (int)lane - row * LPR;
     const int rowc = row < R ? row : 0;  // idle lanes shadow row 0 (results unused)
     const int el = rowc / A, a = rowc - el * A;
@@ -524,14 +525,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 #pragma unroll
             for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
             const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
-            out_st(&b.reward[e], rsum / (float)A);             // torch.mean (:233)
+            out_el(b.reward, e, rsum / (float)A, wt);             // torch.mean (:233)
             float step_num = sn_v + 1.0f;                      // :96
             const bool truncated = step_num > pr.trunc_after;  // :97
             const bool term_old = term_v != 0u;
             const bool terminated = any_col || term_old;       // :213-214
-            out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
-            out_st(&b.terminated[e], (uint8_t)terminated);
-            out_st(&b.truncated[e], (uint8_t)truncated);
+            out_el(b.terminates, e, (uint8_t)(!term_old && all_in), wt);  // :218-219
+            out_el(b.terminated, e, (uint8_t)terminated, wt);
+            out_el(b.truncated, e, (uint8_t)truncated, wt);
             const bool fin = truncated || terminated;          // :102-104
             if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
                 KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -561,12 +562,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                                             (uint64_t)(kl->a.env_offset + e), kl->a.step_idx, s5,
                                             obl, tgl);
                 }
-                for (int i = 0; i < 2 * O; ++i) gob[e * O * 2 + i] = obl[i];
-                gtg[2 * e] = tgl[0];
-                gtg[2 * e + 1] = tgl[1];
+                for (int i = 0; i < 2 * O; ++i) out_el(gob, e * O * 2 + i, obl[i], wt);
+                out_el(gtg, 2 * e, tgl[0], wt);
+                out_el(gtg, 2 * e + 1, tgl[1], wt);
             }
             if (fin) step_num = blend_in(step_num, 0.0f);
-            out_st(&b.step_num[e], step_num);
+            out_el(b.step_num, e, step_num, wt);
             tr_l = truncated;
             co_l = any_col;
             ta_l = all_in;
@@ -737,28 +738,51 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             if (VAL % 16 == 0) {
                 for (int i = (int)lane; i < n / 4; i += 64) {
                     const int rr = i / D4, c4 = i - rr * D4;
-                    out_st4<kNtRows>(gobs + 4 * i, *reinterpret_cast<const float4 *>(src + rr * SP::DP + 4 * c4));
+                    const float4 v = *reinterpret_cast<const float4 *>(src + rr * SP::DP + 4 * c4);
+                    if (kWtOut && wt)
+                        wt_st4(out_buf(gobs, 4u * n), 16u * i, v);
+                    else
+                        out_st4<kNtRows>(gobs + 4 * i, v);
                 }
             } else {
                 for (int i = (int)lane; i < n; i += 64) {
                     const int rr = i / D;
-                    out_st<kNtRows>(gobs + i, src[rr * SP::DP + (i - rr * D)]);
+                    const float v = src[rr * SP::DP + (i - rr * D)];
+                    if (kWtOut && wt)
+                        wt_st(out_buf(gobs, 4u * n), 4u * i, v);
+                    else
+                        out_st<kNtRows>(gobs + i, v);
                 }
             }
         } else if (VAL % 16 == 0 && ne == EPW) {
-            for (int i = (int)lane; i < n / 4; i += 64)
-                out_st4<kNtRows>(gobs + 4 * i, reinterpret_cast<const float4 *>(src)[i]);
+            for (int i = (int)lane; i < n / 4; i += 64) {
+                const float4 v = reinterpret_cast<const float4 *>(src)[i];
+                if (kWtOut && wt)
+                    wt_st4(out_buf(gobs, 4u * n), 16u * i, v);
+                else
+                    out_st4<kNtRows>(gobs + 4 * i, v);
+            }
         } else if (VAL % 8 == 0 && n % 2 == 0) {
-            for (int i = (int)lane; i < n / 2; i += 64)
-                out_st2<kNtRows>(gobs + 2 * i, reinterpret_cast<const float2 *>(src)[i]);
+            for (int i = (int)lane; i < n / 2; i += 64) {
+                const float2 v = reinterpret_cast<const float2 *>(src)[i];
+                if (kWtOut && wt)
+                    wt_st2(out_buf(gobs, 4u * n), 8u * i, v);
+                else
+                    out_st2<kNtRows>(gobs + 2 * i, v);
+            }
         } else {
-            for (int i = (int)lane; i < n; i += 64) out_st<kNtRows>(gobs + i, src[i]);
+            for (int i = (int)lane; i < n; i += 64) {
+                if (kWtOut && wt)
+                    wt_st(out_buf(gobs, 4u * n), 4u * i, src[i]);
+                else
+                    out_st<kNtRows>(gobs + i, src[i]);
+            }
         }
         if (gnorm)
 #pragma unroll 8  // (mean/scale loads of 8 iterations in flight at once)
             for (int i = (int)lane; i < n; i += 64) {
                 const int rr = i / D, kk = i - rr * D;
-                gnorm[i] = (src[rr * SP::DP + kk] - mean[kk]) / scale[kk];
+                out_el(gnorm, (int64_t)i, (src[rr * SP::DP + kk] - mean[kk]) / scale[kk], wt);
             }
     }
     if (!OBS_ONLY) {
@@ -766,10 +790,20 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         const int n = nr * 5;
         constexpr int SAL = gcd_c(R * 20, 16);
         if (SAL % 16 == 0 && ne == EPW) {
-            for (int i = (int)lane; i < n / 4; i += 64)
-                out_st4<kNtRows>(gst + 4 * i, reinterpret_cast<const float4 *>(st)[i]);
+            for (int i = (int)lane; i < n / 4; i += 64) {
+                const float4 v = reinterpret_cast<const float4 *>(st)[i];
+                if (kWtOut && wt)
+                    wt_st4(out_buf(gst, 4u * n), 16u * i, v);
+                else
+                    out_st4<kNtRows>(gst + 4 * i, v);
+            }
         } else {
-            for (int i = (int)lane; i < n; i += 64) out_st<kNtRows>(gst + i, st[i]);
+            for (int i = (int)lane; i < n; i += 64) {
+                if (kWtOut && wt)
+                    wt_st(out_buf(gst, 4u * n), 4u * i, st[i]);
+                else
+                    out_st<kNtRows>(gst + i, st[i]);
+            }
         }
     }
     STAMP(6);

@@ -15,6 +15,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
     const int A = A_T ? A_T : args.A;
     const int O = O_T ? O_T : args.O;
     const int S = args.S, W = args.W;
+    const bool wt = (pr.flags & kWriteThroughFlag) != 0;  // written-through outputs
     constexpr int D_T = static_obs_dim(A_T, O_T);
     constexpr bool REGROW = D_T > 0 && D_T <= kRowRegsMaxD;
     const WavePlan wp = make_plan(W, A, O, S, REGROW);
@@ -133,15 +134,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                 }
                 const float *rr = all_in ? rhit : rmiss;
                 const float rsum = torch_row_sum(rr + lane * A, A, [](float r) { return r; });
-                out_st(&b.reward[e], rsum / (float)A);                     // torch.mean (:233)
+                out_el(b.reward, e, rsum / (float)A, wt);                     // torch.mean (:233)
 
                 float step_num = step_num_in + 1.0f;               // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = term_in != 0;
                 const bool terminated = any_col || term_old;       // :213-214
-                out_st(&b.terminates[e], (uint8_t)(!term_old && all_in));  // :218-219
-                out_st(&b.terminated[e], (uint8_t)terminated);
-                out_st(&b.truncated[e], (uint8_t)truncated);
+                out_el(b.terminates, e, (uint8_t)(!term_old && all_in), wt);  // :218-219
+                out_el(b.terminated, e, (uint8_t)terminated, wt);
+                out_el(b.truncated, e, (uint8_t)truncated, wt);
                 fin = truncated || terminated;                     // :102-104
                 if (fin) {
                     float *sts = st + 5 * A * lane;
@@ -165,7 +166,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                     b.target[2 * e + 1] = tge[1];
                     step_num = blend_in(step_num, 0.0f);
                 }
-                out_st(&b.step_num[e], step_num);
+                out_el(b.step_num, e, step_num, wt);
                 envbits[lane] = fin ? 1u : 0u;
                 tr_l = truncated;
                 co_l = any_col;
@@ -200,24 +201,24 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
         // ---- stream the tile out
         if constexpr (REGROW) {
             if (row_on) {
-                store_row<D_T>(b.obs + (e0 * A + lane) * D_T, rowv);
+                store_row<D_T>(b.obs + (e0 * A + lane) * D_T, rowv, wt);
                 if (norm) {
                     float nv[D_T];
 #pragma unroll
                     for (int k = 0; k < D_T; ++k)
                         nv[k] = (rowv[k] - b.norm_mean[k]) / b.norm_scale[k];
-                    store_row<D_T>(b.obs_norm + (e0 * A + lane) * D_T, nv);
+                    store_row<D_T>(b.obs_norm + (e0 * A + lane) * D_T, nv, wt);
                 }
             }
         } else if (wp.obs_lds)
             wave_store(b.obs + e0 * A * D, obs_t, nr * D, lane,
-                       norm ? b.obs_norm + e0 * A * D : nullptr, b.norm_mean, b.norm_scale, D);
+                       norm ? b.obs_norm + e0 * A * D : nullptr, b.norm_mean, b.norm_scale, D, wt);
         else if (norm && row_on)
             for (int k = 0; k < D; ++k)
                 b.obs_norm[(e0 * A + lane) * D + k] =
                     (out_row[k] - b.norm_mean[k]) / b.norm_scale[k];
         if (!OBS_ONLY)
-            wave_store(b.states + e0 * A * 5, st, nr * 5, lane, nullptr, nullptr, nullptr, 1);
+            wave_store(b.states + e0 * A * 5, st, nr * 5, lane, nullptr, nullptr, nullptr, 1, wt);
         STAMP(6);
     }
     if (!OBS_ONLY && b.counters && lane == 0) {

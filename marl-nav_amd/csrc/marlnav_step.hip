@@ -463,10 +463,17 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
 {
     if (!pr_in) return fail(MARLNAV_EINVAL, "params/buffers is NULL");
     MarlnavParams prm = *pr_in;
-    prm.flags &= ~kTermsFastFlag;
+    prm.flags &= ~(kTermsFastFlag | kWriteThroughFlag);
     if (terms_fast_params(prm)) prm.flags |= kTermsFastFlag;
     const MarlnavParams *pr = &prm;
     if (int rc = validate(d)) return rc;
+    // written-through outputs (device_math.h kWriteThroughFlag) for launches
+    // that write at least kWriteThroughMinBytes
+    {
+        const int64_t A = d->num_agents, D = obs_dim(d->num_agents, d->num_obstacles);
+        const int64_t wbytes = (int64_t)d->num_parallel * (20 * A + 4 * A * D + 11);
+        if (wbytes >= kWriteThroughMinBytes) prm.flags |= kWriteThroughFlag;
+    }
     if (!pr || !b) return fail(MARLNAV_EINVAL, "params/buffers is NULL");
     if (!b->states || !b->obstacles || !b->target || !b->step_num || !b->terminates ||
         !b->actions || !b->obs || !b->reward || !b->terminated || !b->truncated)
@@ -517,6 +524,9 @@ int marlnav_observe(const MarlnavDims *d, const MarlnavParams *params, const flo
     // the angle cap (environment.py:172-177) is the only parameter observe reads;
     // NULL params: the reference's default (environment.py:65)
     pr.cap_distance = params ? params->cap_distance : 0.1f;
+    if ((int64_t)d->num_parallel * d->num_agents * obs_dim(d->num_agents, d->num_obstacles) * 4 >=
+        kWriteThroughMinBytes)
+        pr.flags |= kWriteThroughFlag;
     const bool fsplit = g_family == MARLNAV_FAMILY_SPLIT;
     if (family_allowed(MARLNAV_FAMILY_SPLIT))
         if (const SplitVariant *v = select_split(d, args.b, true, fsplit)) {
