@@ -76,6 +76,9 @@ struct OutSet {
     }
 };
 
+// tensors of the Env that a step writes in place (track_state)
+constexpr int kHeld = 5;
+
 struct Engine {
     PyObject_HEAD
     MarlnavDims dims;
@@ -97,17 +100,18 @@ struct Engine {
     std::vector<OutSet *> *pool;
     int next;
     OutSet *last;                 // the set the previous step returned
-    // the Env's states / obstacles / target tensors (strong refs,
-    // track_state): a step may not write them in place while anything else
-    // refers to them
-    PyObject *held[3];
-    c10::Storage held_st[3];
+    // the Env's states / obstacles / target / step_num / terminates tensors
+    // (strong refs, track_state): a step may not write them in place while
+    // anything else refers to them
+    PyObject *held[kHeld];
+    c10::Storage held_st[kHeld];
 };
 
-// The reference's re-init rebinds `states`, `obstacles` and `target` to new
-// tensors (environment.py:79-81), so a caller holding the old tensor keeps
-// its pre-re-init values (for `states`: the moved ones, :113-123 move in
-// place). Here the step kernel writes them in place, so the step goes
+// The reference's re-init rebinds `states`, `obstacles`, `target` and
+// `_step_num` to new tensors (environment.py:79-83) and `_terminates` at
+// :219, so a caller holding the old tensor keeps its pre-step values (for
+// `states`: the moved ones, :113-123 move in place; for `_step_num`: +1, the
+// in-place increment of :96). Here the step kernel writes them in place, so the step goes
 // through Env._step_py, which gives the Env fresh copies first, whenever a
 // tensor is referenced beyond the Env's attribute and this engine (2 Python
 // references) or its storage is viewed by another tensor (use count beyond
@@ -119,12 +123,14 @@ bool state_shared(const Engine *e, int i)
 
 bool any_state_shared(const Engine *e)
 {
-    return state_shared(e, 0) || state_shared(e, 1) || state_shared(e, 2);
+    for (int i = 0; i < kHeld; ++i)
+        if (state_shared(e, i)) return true;
+    return false;
 }
 
 void release_state(Engine *e)
 {
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < kHeld; ++i) {
         Py_CLEAR(e->held[i]);
         e->held_st[i] = c10::Storage();
     }
@@ -353,7 +359,7 @@ int Engine_init(Engine *e, PyObject *args, PyObject *)
     e->steps_done = 0;
     e->next = 0;
     e->last = nullptr;
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < kHeld; ++i) {
         e->held[i] = nullptr;
         new (&e->held_st[i]) c10::Storage();
     }
@@ -365,7 +371,7 @@ void Engine_dealloc(Engine *e)
     clear_pool(e);
     delete e->pool;
     release_state(e);
-    for (int i = 0; i < 3; ++i) e->held_st[i].~Storage();
+    for (int i = 0; i < kHeld; ++i) e->held_st[i].~Storage();
     Py_CLEAR(e->stream_fn);
     Py_CLEAR(e->dev_index);
     Py_CLEAR(e->factory);
@@ -451,18 +457,20 @@ PyObject *Engine_launch(Engine *e, PyObject *args)
     return do_launch(e, (const void *)act, fp, extra);
 }
 
-// track_state(states, obstacles, target): the Env's current tensors
+// track_state(states, obstacles, target, step_num, terminates): the Env's
+// current tensors
 PyObject *Engine_track_state(Engine *e, PyObject *args)
 {
-    PyObject *o[3];
-    if (!PyArg_ParseTuple(args, "OOO", &o[0], &o[1], &o[2])) return nullptr;
-    for (int i = 0; i < 3; ++i)
+    PyObject *o[kHeld];
+    if (!PyArg_ParseTuple(args, "OOOOO", &o[0], &o[1], &o[2], &o[3], &o[4])) return nullptr;
+    for (int i = 0; i < kHeld; ++i)
         if (!THPVariable_Check(o[i])) {
-            PyErr_SetString(PyExc_TypeError, "track_state(states, obstacles, target): tensors");
+            PyErr_SetString(PyExc_TypeError,
+                            "track_state(states, obstacles, target, step_num, terminates): tensors");
             return nullptr;
         }
     release_state(e);
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < kHeld; ++i) {
         Py_INCREF(o[i]);
         e->held[i] = o[i];
         e->held_st[i] = THPVariable_Unpack(o[i]).storage();
@@ -470,12 +478,16 @@ PyObject *Engine_track_state(Engine *e, PyObject *args)
     Py_RETURN_NONE;
 }
 
-// (states_shared, obstacles_shared, target_shared)
+// one flag per tracked tensor: (states, obstacles, target, step_num, terminates)
 PyObject *Engine_shared_state(Engine *e, PyObject *)
 {
-    return Py_BuildValue("(OOO)", state_shared(e, 0) ? Py_True : Py_False,
-                         state_shared(e, 1) ? Py_True : Py_False,
-                         state_shared(e, 2) ? Py_True : Py_False);
+    PyObject *t = PyTuple_New(kHeld);
+    for (int i = 0; i < kHeld; ++i) {
+        PyObject *b = state_shared(e, i) ? Py_True : Py_False;
+        Py_INCREF(b);
+        PyTuple_SET_ITEM(t, i, b);
+    }
+    return t;
 }
 
 PyObject *Engine_reset_pool(Engine *e, PyObject *)
@@ -510,7 +522,8 @@ PyMethodDef Engine_methods[] = {
      "launch(actions_ptr, fresh_ptrs|None, extra_flags) -> (obs, reward, terminated, truncated)"},
     {"reset_pool", (PyCFunction)Engine_reset_pool, METH_NOARGS, "drop every pooled output set"},
     {"track_state", (PyCFunction)Engine_track_state, METH_VARARGS,
-     "track_state(states, obstacles, target): the tensors a step must not write while shared"},
+     "track_state(states, obstacles, target, step_num, terminates): the tensors a step must not "
+     "write while shared"},
     {"shared_state", (PyCFunction)Engine_shared_state, METH_NOARGS,
      "(states_shared, obstacles_shared, target_shared)"},
     {"last_finished", (PyCFunction)Engine_last_finished, METH_NOARGS,

@@ -408,7 +408,11 @@ __global__ void __launch_bounds__(64 * A)
     }
     STAMP(5);
     if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
-        if (!(MARLNAV_AB & 2))
+        if (MARLNAV_AB & 4096)
+            block_store2<E * A * D, 4, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)), st, tid, wt);
+        else if (MARLNAV_AB & 8192)
+            block_store2<4, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)), st, tid, wt);
+        else if (!(MARLNAV_AB & 2))
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
                                                st, tid, wt);  // (E = 64: whole 16-byte pieces)
     } else if (!OBS_ONLY && full && NT % D == 0) {

@@ -82,7 +82,7 @@ struct FlatFinList {
 // Finished envs re-initialised and re-observed by the whole workgroup
 // (after one block barrier) instead of by their own wave: pays where an
 // env's re-observation is long (measured: A3/O8 and A16/O32 faster, A3/O3
-// slower). MARLNAV_SPLIT_SPREAD=0 turns it off (A/B builds).
+// slower).
 template <int A, int O>
 constexpr bool kSplitSpread = A * (1 + O + (A - 1)) >= 32;
 

@@ -33,6 +33,8 @@
 // acosf.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -401,10 +403,16 @@ int launch(StepFn fn, const Launch &L, StepArgs args, MarlnavParams pr, void *st
 }
 
 // marlnav_debug_force_family / marlnav_debug_last_family (testing hooks)
-int g_family = MARLNAV_FAMILY_AUTO;
+// (a testing hook: atomic, so a test thread forcing a family never races a
+// stepping thread's read)
+std::atomic<int> g_family{MARLNAV_FAMILY_AUTO};
 thread_local int g_last_family = MARLNAV_FAMILY_AUTO;
 
-bool family_allowed(int f) { return g_family == MARLNAV_FAMILY_AUTO || g_family == f; }
+bool family_allowed(int f)
+{
+    const int g = g_family.load(std::memory_order_relaxed);
+    return g == MARLNAV_FAMILY_AUTO || g == f;
+}
 
 }  // namespace
 
@@ -414,10 +422,10 @@ int marlnav_abi_version(void) { return MARLNAV_ABI_VERSION; }
 
 int marlnav_debug_force_family(int family)
 {
-    const int prev = g_family;
+    const int prev = g_family.load(std::memory_order_relaxed);
     if (family < MARLNAV_FAMILY_AUTO || family > MARLNAV_FAMILY_WAVE)
         return fail(MARLNAV_EINVAL, "unknown kernel family %d", family);
-    g_family = family;
+    g_family.store(family, std::memory_order_relaxed);
     return prev;
 }
 
@@ -491,7 +499,7 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
     args.b = *b;
     args.step_idx = step_idx;
     const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
-    const bool fsplit = g_family == MARLNAV_FAMILY_SPLIT;
+    const bool fsplit = g_family.load(std::memory_order_relaxed) == MARLNAV_FAMILY_SPLIT;
     if (family_allowed(MARLNAV_FAMILY_SPLIT))
         if (const SplitVariant *v = select_split(d, *b, false, fsplit)) {
             g_last_family = MARLNAV_FAMILY_SPLIT;
@@ -527,7 +535,7 @@ int marlnav_observe(const MarlnavDims *d, const MarlnavParams *params, const flo
     if ((int64_t)d->num_parallel * d->num_agents * obs_dim(d->num_agents, d->num_obstacles) * 4 >=
         kWriteThroughMinBytes)
         pr.flags |= kWriteThroughFlag;
-    const bool fsplit = g_family == MARLNAV_FAMILY_SPLIT;
+    const bool fsplit = g_family.load(std::memory_order_relaxed) == MARLNAV_FAMILY_SPLIT;
     if (family_allowed(MARLNAV_FAMILY_SPLIT))
         if (const SplitVariant *v = select_split(d, args.b, true, fsplit)) {
             g_last_family = MARLNAV_FAMILY_SPLIT;

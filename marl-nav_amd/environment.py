@@ -212,7 +212,13 @@ class Env(object):
             torch._C._cuda_getCurrentRawStream, self.device.index,
             lambda: _new_output_set(wr()), lambda a: wr()._step_py(a))
         object.__setattr__(self, '_engine', eng)
-        object.__setattr__(self, 'step', eng)   # Env.step: the engine's fast path
+        if type(self).step is Env.step:
+            # Env.step: the engine's fast path, bound on the instance. A
+            # subclass that overrides step keeps its method (which reaches
+            # the engine through super().step); replacing Env.step on the
+            # class after construction does not reach instances already
+            # built.
+            object.__setattr__(self, 'step', eng)
         self._reinit_mask = torch.zeros(P, device=self.device)
         self._configure()
 
@@ -261,28 +267,45 @@ class Env(object):
         fast = (not self._params_dirty and self._rng == 'native'
                 and self._init_sampler is self._default_init_sampler)
         eng.configure(bytes(self._dims), bytes(self._cparams), bytes(b), fast)
-        eng.track_state(self._states, self._obstacles, self._target)
+        eng.track_state(self._states, self._obstacles, self._target,
+                        self.__dict__['_step_num_t'], self.__dict__['_terminates_t'])
 
     def _unshare_state(self):
-        """Copy-on-write of the state tensors. The reference's re-init
-        rebinds `states`, `obstacles` and `target` to new tensors
-        (environment.py:79-81), so a caller still holding one from before a
-        step keeps its values - for `states` the moved ones, since
-        `_move_agents` writes it in place first (:113-123). The kernel writes
-        all three in place; when the engine reports one referenced outside
-        the Env, the Env moves to a copy (stream-ordered) before the step.
-        Returns the held pre-step `states` tensor (for `_move_held`) or None."""
-        st_shared, ob_shared, tg_shared = self._engine.shared_state()
-        held = None
-        if st_shared:
+        """Copy-on-write of the tensors a step writes in place. The
+        reference's re-init rebinds `states`, `obstacles`, `target` and
+        `_step_num` to new tensors (environment.py:79-83) and `_terminates` at
+        :219, so a caller still holding one from before a step keeps its
+        values - for `states` the moved ones, since `_move_agents` writes it
+        in place first (:113-123), and for `_step_num` the incremented ones
+        (:96, in place). The kernel writes all five in place; when the engine
+        reports one referenced outside the Env, the Env moves to a copy
+        (stream-ordered) before the step. Returns (held pre-step `states` or
+        None, held pre-step `_step_num` or None) for `_finish_held`."""
+        shared = self._engine.shared_state()
+        held = held_sn = None
+        if shared[0]:
             held = self._states
             object.__setattr__(self, '_states', held.clone())
-        if ob_shared:
+        if shared[1]:
             object.__setattr__(self, '_obstacles', self._obstacles.clone())
-        if tg_shared:
+        if shared[2]:
             object.__setattr__(self, '_target', self._target.clone())
+        if shared[3]:
+            held_sn = self.__dict__['_step_num_t']
+            self.__dict__['_step_num_t'] = held_sn.clone()
+        if shared[4]:
+            self.__dict__['_terminates_t'] = self.__dict__['_terminates_t'].clone()
         self._configure()
-        return held
+        return held, held_sn
+
+    def _finish_held(self, held, actions_ptr):
+        """What a holder of a pre-step tensor sees after the reference's step:
+        the moved `states` (:113-123) and `_step_num` + 1 (:96)."""
+        held_st, held_sn = held
+        if held_st is not None:
+            self._move_held(held_st, actions_ptr)
+        if held_sn is not None:
+            held_sn.add_(1.0)
 
     def _move_held(self, held, actions_ptr):
         """The reference's in-place `_move_agents` (environment.py:113-123) on
@@ -370,6 +393,7 @@ class Env(object):
         self._split = [1, 1, O, O, self.num_agents - 1, self.num_agents - 1]
         eng = self.__dict__.get('_engine')
         if eng is not None:
+            self._keep_reinit_mask()
             eng.reset_pool()               # output shapes may have changed
         if hasattr(self, '_counters') and old != (d.num_agents, d.num_obstacles, S):
             totals = self._counter_totals()
@@ -467,6 +491,13 @@ class Env(object):
                 self.__dict__['_reinit_mask_at'] = eng.steps_done
         return self.__dict__.get('_reinit_mask_t')
 
+    def _keep_reinit_mask(self):
+        """Build `_reinit_mask` from the last step's flags before the engine
+        drops its output sets (reset_pool), which hold them."""
+        eng = self.__dict__.get('_engine')
+        if eng is not None and eng.steps_done:
+            self._reinit_mask   # noqa: B018 (materialises the cached mask)
+
     @_reinit_mask.setter
     def _reinit_mask(self, value):
         self.__dict__['_reinit_mask_t'] = value
@@ -513,6 +544,7 @@ class Env(object):
         """Have every step also write ``normalizer``'s output (utils.py:519-532)
         from the kernel; ``normalizer(obs)`` then returns it without work."""
         self._normalizer = normalizer
+        self._keep_reinit_mask()
         self._engine.reset_pool()
         if normalizer is None:
             self._obs_norm_buffers = None
@@ -592,7 +624,7 @@ class Env(object):
         modes (the host init sampler is called every step, environment.py:78)."""
         if self._params_dirty:
             self._sync_params()
-        held = self._unshare_state() if any(self._engine.shared_state()) else None
+        held = self._unshare_state() if any(self._engine.shared_state()) else (None, None)
         dev = self.device
         if not (type(actions) is torch.Tensor and actions.dtype is _F32
                 and actions.device == dev and actions.shape == self._act_shape
@@ -604,8 +636,7 @@ class Env(object):
             if not eng.fast_ok:
                 self._configure()
             out = eng.launch(actions.data_ptr(), None, 0)
-            if held is not None:
-                self._move_held(held, actions.data_ptr())
+            self._finish_held(held, actions.data_ptr())
             return out
         P = self.num_parallel
         fs, fo, ft = self._init_sampler()                # environment.py:78
@@ -629,8 +660,7 @@ class Env(object):
             if isinstance(init, MockInitializer):
                 init.states = self._states.clone()
         del keep   # stream-ordered: the caching allocator reuses them after the kernel
-        if held is not None:
-            self._move_held(held, actions.data_ptr())
+        self._finish_held(held, actions.data_ptr())
         return out
 
 

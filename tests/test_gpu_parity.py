@@ -427,6 +427,99 @@ def test_held_states_reference_rng_mode(pkg):
     assert not torch.equal(held, env.states)
 
 
+def test_held_states_pair_split_kernel(pkg):
+    """The held-`states` rule on the pair-split kernel family (A16/O32, the
+    configs[3] shape; test_held_state_tensors_see_what_the_reference_shows
+    covers the env-block kernel): a held pre-step `states` receives the
+    moved states of a step in which every env truncates, the Env's own
+    tensor the re-initialised ones."""
+    P, A, O = 60, 16, 32
+    env = make_env(pkg, P, A, O, episode_len=2)
+    acts = torch.rand(P, A, 2, device=DEV) - 0.5
+    env.step(acts)
+    assert env._lib.marlnav_debug_last_family() == 2   # MARLNAV_FAMILY_SPLIT
+    held, held0 = env.states, env.states.clone()
+    ob_k, tg_k = env.obstacles.clone(), env.target.clone()
+    env.step(acts)                      # step 2: every env truncates
+    mv = make_env(pkg, P, A, O, episode_len=10 ** 9)
+    mv._ob_coll_dist = mv._ag_coll_dist = float("-inf")
+    mv.states, mv.obstacles, mv.target = held0, ob_k, tg_k
+    mv.step(acts)
+    torch.cuda.synchronize()
+    assert torch.equal(held, mv.states)
+    assert not torch.equal(held, env.states)
+
+
+def test_held_step_num_and_terminates_see_what_the_reference_shows(pkg):
+    """`_step_num` is incremented in place (environment.py:96) and then
+    rebound by the re-init (:83); `_terminates` is rebound at :219. A caller
+    holding either from before a step sees the reference's: step_num + 1 for
+    every env (finished ones included), the old terminates flags; the Env's
+    own tensors carry on as in a run without holders."""
+    P = 4096 + 3
+    env = make_env(pkg, P, 3, 3, episode_len=3)
+    twin = make_env(pkg, P, 3, 3, episode_len=3)
+    acts = [torch.rand(P, 3, 2, device=DEV) - 0.5 for _ in range(3)]
+    for k in range(2):
+        env.step(acts[k])
+        twin.step(acts[k])
+    sn, tm = env._step_num, env._terminates
+    sn0, tm0 = sn.clone(), tm.clone()
+    env.step(acts[2])                   # step 3: every env truncates
+    twin.step(acts[2])
+    torch.cuda.synchronize()
+    assert torch.equal(sn, sn0 + 1.0) and torch.equal(tm, tm0)
+    assert torch.equal(env._step_num, twin._step_num)
+    assert torch.equal(env._terminates, twin._terminates)
+    assert float(env._step_num.max()) == 0.0        # re-initialised: rebound to zeros
+    assert torch.equal(env.states, twin.states)
+
+
+def test_reinit_mask_survives_state_assignment(pkg):
+    """`_reinit_mask` (environment.py:102-103) is the last step's
+    where(truncated | terminated, 1, 0) even after an assignment that drops
+    the engine's output sets (states, obstacles, target, a normaliser)."""
+    P = 300
+    env = make_env(pkg, P, 3, 3, episode_len=2)
+    acts = torch.rand(P, 3, 2, device=DEV) - 0.5
+    env.step(acts)
+    _, _, term, trunc = env.step(acts)       # step 2: every env truncates
+    want = torch.where(torch.logical_or(trunc, term), 1, 0)
+    del term, trunc
+    env.states = env.states.clone()
+    assert torch.equal(env._reinit_mask, want)
+    env.obstacles = env.obstacles.clone()
+    assert torch.equal(env._reinit_mask, want) and int(want.sum()) == P
+
+
+def test_subclass_step_override_is_called(pkg):
+    """A subclass overriding step keeps its method (the engine binds itself
+    on the instance only for Env's own step) and reaches the native step
+    through super().step."""
+    base = pkg.Env
+
+    class Scaled(base):
+        calls = 0
+
+        def step(self, actions):
+            Scaled.calls += 1
+            obs, rew, term, trunc = super().step(actions)
+            return obs, rew * 2.0, term, trunc
+
+    P = 200
+    args = cli_args(num_parallel=P, episode_len=50)
+    params = pkg.set_env_params(args, DEV)
+    params.update(rng="native", seed=7)
+    sub, ref = Scaled(params), base(params)
+    acts = torch.rand(P, 3, 2, device=DEV) - 0.5
+    for _ in range(3):
+        _, r1, _, _ = sub.step(acts)
+        _, r0, _, _ = ref.step(acts)
+        assert torch.equal(r1, r0 * 2.0)
+    assert Scaled.calls == 3
+    assert "step" not in sub.__dict__ and "step" in ref.__dict__
+
+
 def test_discounted_returns_match_reference_and_oracle(pkg):
     """§8(f) row 3: the device scan against MAPPO._process_rewards run
     unmodified (F5) and the C oracle at rollout size; float64 within 1e-12."""

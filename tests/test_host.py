@@ -104,10 +104,11 @@ def test_engine_fast_path_falls_back_for_other_actions():
 
 
 def test_engine_reports_held_state_tensors():
-    """Copy-on-write rule for states / obstacles / target (environment.py:
-    79-81 rebind them): a tracked tensor counts as held once
-    anything beyond its owner's attribute and the engine refers to it, or a
-    view shares its storage; a held tensor keeps steps off the fast path."""
+    """Copy-on-write rule for states / obstacles / target / step_num /
+    terminates (environment.py:79-83 and :219 rebind them): a
+    tracked tensor counts as held once anything beyond its owner's attribute
+    and the engine refers to it, or a view shares its storage; a held tensor
+    keeps steps off the fast path."""
     calls = []
     eng, cb = _cpu_engine(calls)
 
@@ -115,24 +116,66 @@ def test_engine_reports_held_state_tensors():
         pass
     o = Owner()
     o.s, o.ob, o.tg = torch.zeros(10, 3, 5), torch.zeros(10, 3, 2), torch.zeros(10, 1, 2)
-    eng.track_state(o.s, o.ob, o.tg)
-    assert eng.shared_state() == (False, False, False)
+    o.sn, o.tm = torch.zeros(10), torch.zeros(10, dtype=torch.bool)
+    track = lambda: eng.track_state(o.s, o.ob, o.tg, o.sn, o.tm)  # noqa: E731
+    none = (False,) * 5
+    track()
+    assert eng.shared_state() == none
     s = o.s
-    assert eng.shared_state() == (True, False, False)
+    assert eng.shared_state() == (True, False, False, False, False)
     del s
     v = o.tg[:, 0]
-    assert eng.shared_state() == (False, False, True)
+    assert eng.shared_state() == (False, False, True, False, False)
     del v
     lst = [o.ob]
-    assert eng.shared_state() == (False, True, False)
+    assert eng.shared_state() == (False, True, False, False, False)
     del lst
-    assert eng.shared_state() == (False, False, False)
+    sn = o.sn
+    assert eng.shared_state() == (False, False, False, True, False)
+    del sn
+    tm = o.tm[3:]
+    assert eng.shared_state() == (False, False, False, False, True)
+    del tm
+    assert eng.shared_state() == none
     # re-tracking releases the old tensors
     old = o.s
     o.s = o.s.clone()
-    eng.track_state(o.s, o.ob, o.tg)
-    assert eng.shared_state() == (False, False, False)
+    track()
+    assert eng.shared_state() == none
     del old
+
+
+def test_dlpack_export_counts_as_a_holder():
+    """INTEGRATION.md's holder contract: a raw-pointer consumer must hold a
+    tensor reference. A DLPack export (torch.utils.dlpack.to_dlpack) does -
+    its capsule keeps the storage - so an exported output set is not
+    recycled and an exported state tensor is not written in place, until the
+    capsule is gone."""
+    from torch.utils.dlpack import to_dlpack
+    calls = []
+    eng, cb = _cpu_engine(calls)
+    out = eng.launch(0, None, 0)
+    cap = to_dlpack(out[0]._packed)
+    ptr = calls[-1][0]
+    del out
+    for _ in range(6):
+        eng.launch(0, None, 0)
+        assert calls[-1][0] != ptr
+    del cap
+    eng.launch(0, None, 0)
+    eng.launch(0, None, 0)
+    assert ptr in [c[0] for c in calls[-2:]]
+
+    class Owner:
+        pass
+    o = Owner()
+    o.s, o.ob, o.tg = torch.zeros(10, 3, 5), torch.zeros(10, 3, 2), torch.zeros(10, 1, 2)
+    o.sn, o.tm = torch.zeros(10), torch.zeros(10, dtype=torch.bool)
+    eng.track_state(o.s, o.ob, o.tg, o.sn, o.tm)
+    cap = to_dlpack(o.s)
+    assert eng.shared_state()[0]
+    del cap
+    assert not eng.shared_state()[0]
 
 
 def test_cli_mirrors_reference_arguments():
