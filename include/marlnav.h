@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MARLNAV_ABI_VERSION 3
+#define MARLNAV_ABI_VERSION 4
 
 /* error codes */
 #define MARLNAV_OK 0
@@ -129,6 +129,12 @@ typedef struct MarlnavStepBuffers {
      * old value finite) take their target and agent-agent pairs from it and
      * compute only the agent-obstacle pairs. */
     const float *formation_obs; /* (A, A, 2)                               */
+    /* optional second state buffer (NULL: `states` is updated in place): the
+     * step reads `states` and writes every env's new state row here, so the
+     * launch never writes the lines it read (a host double-buffers the two,
+     * as the reference rebinds `states` each step, environment.py:80).
+     * Must not overlap `states`. */
+    float *states_out;       /* (P, A, 5)                                  */
 } MarlnavStepBuffers;
 
 /* Env.step(actions) - environment.py:92-107 (with _move_agents :113-137,

@@ -11,7 +11,7 @@ fallback: if the library is missing or fails to load, ``load_library`` raises.
 import ctypes
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 FRESH_STATES_FROM_MOVED = 0x1
 NOISY_AGENTS = 0x2
@@ -53,7 +53,7 @@ STEP_BUFFER_FIELDS = (
     "states", "obstacles", "target", "step_num", "terminates", "actions",
     "fresh_states", "fresh_obstacles", "fresh_target", "formation", "obs",
     "reward", "terminated", "truncated", "counters", "obs_norm", "norm_mean",
-    "norm_scale", "formation_obs")
+    "norm_scale", "formation_obs", "states_out")
 
 
 class MarlnavStepBuffers(ctypes.Structure):

@@ -30,6 +30,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "../../include/marlnav.h"
@@ -76,8 +77,14 @@ struct OutSet {
     }
 };
 
-// tensors of the Env that a step writes in place (track_state)
-constexpr int kHeld = 5;
+// tensors of the Env that a step writes (track_state): states, obstacles,
+// target, step_num, terminates, and the second states buffer
+constexpr int kHeld = 6;
+constexpr int kStates = 0, kStatesAlt = 5;
+// Python references a tracked tensor has when nothing outside the Env holds
+// it: the Env attribute and this engine, except the two state buffers, which
+// only the engine holds (Env.states asks the engine for the current one)
+constexpr Py_ssize_t kOwnRefs[kHeld] = {1, 2, 2, 2, 2, 1};
 
 struct Engine {
     PyObject_HEAD
@@ -118,7 +125,8 @@ struct Engine {
 // the tensor's own and this engine's copy).
 bool state_shared(const Engine *e, int i)
 {
-    return e->held[i] && (Py_REFCNT(e->held[i]) > 2 || e->held_st[i].use_count() > 2);
+    return e->held[i] &&
+           (Py_REFCNT(e->held[i]) > kOwnRefs[i] || e->held_st[i].use_count() > 2);
 }
 
 bool any_state_shared(const Engine *e)
@@ -316,6 +324,13 @@ PyObject *do_launch(Engine *e, const void *actions, const MarlnavStepBuffers *fr
         }
         return raise_step_error(e, rc);
     }
+    if (b.states_out && e->held[kStatesAlt]) {
+        // the step wrote the new states into the second buffer: it is the
+        // current one from here on
+        std::swap(e->held[kStates], e->held[kStatesAlt]);
+        std::swap(e->held_st[kStates], e->held_st[kStatesAlt]);
+        std::swap(e->base.states, e->base.states_out);
+    }
     e->step_idx++;
     e->steps_done++;
     if (e->last != s) forget_last(e);
@@ -457,25 +472,52 @@ PyObject *Engine_launch(Engine *e, PyObject *args)
     return do_launch(e, (const void *)act, fp, extra);
 }
 
-// track_state(states, obstacles, target, step_num, terminates): the Env's
-// current tensors
+// track_state(states, obstacles, target, step_num, terminates, states_alt):
+// the Env's current tensors; states_alt (or None) is the buffer the next step
+// writes the new states into (MarlnavStepBuffers.states_out), after which
+// the two state buffers swap roles (double-buffered states: the step never
+// writes the lines it read)
 PyObject *Engine_track_state(Engine *e, PyObject *args)
 {
     PyObject *o[kHeld];
-    if (!PyArg_ParseTuple(args, "OOOOO", &o[0], &o[1], &o[2], &o[3], &o[4])) return nullptr;
+    if (!PyArg_ParseTuple(args, "OOOOOO", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5]))
+        return nullptr;
     for (int i = 0; i < kHeld; ++i)
-        if (!THPVariable_Check(o[i])) {
+        if (!THPVariable_Check(o[i]) && !(i == kStatesAlt && o[i] == Py_None)) {
             PyErr_SetString(PyExc_TypeError,
-                            "track_state(states, obstacles, target, step_num, terminates): tensors");
+                            "track_state(states, obstacles, target, step_num, terminates, "
+                            "states_alt|None): tensors");
             return nullptr;
         }
     release_state(e);
     for (int i = 0; i < kHeld; ++i) {
+        if (o[i] == Py_None) continue;
         Py_INCREF(o[i]);
         e->held[i] = o[i];
         e->held_st[i] = THPVariable_Unpack(o[i]).storage();
     }
+    e->base.states = e->held[kStates] ? (float *)THPVariable_Unpack(e->held[kStates]).data_ptr()
+                                      : e->base.states;
+    e->base.states_out = e->held[kStatesAlt]
+                             ? (float *)THPVariable_Unpack(e->held[kStatesAlt]).data_ptr()
+                             : nullptr;
     Py_RETURN_NONE;
+}
+
+// the current states tensor (new reference), or None
+PyObject *Engine_states(Engine *e, PyObject *)
+{
+    PyObject *t = e->held[kStates] ? e->held[kStates] : Py_None;
+    Py_INCREF(t);
+    return t;
+}
+
+// the second states buffer (new reference), or None
+PyObject *Engine_states_alt(Engine *e, PyObject *)
+{
+    PyObject *t = e->held[kStatesAlt] ? e->held[kStatesAlt] : Py_None;
+    Py_INCREF(t);
+    return t;
 }
 
 // one flag per tracked tensor: (states, obstacles, target, step_num, terminates)
@@ -522,10 +564,13 @@ PyMethodDef Engine_methods[] = {
      "launch(actions_ptr, fresh_ptrs|None, extra_flags) -> (obs, reward, terminated, truncated)"},
     {"reset_pool", (PyCFunction)Engine_reset_pool, METH_NOARGS, "drop every pooled output set"},
     {"track_state", (PyCFunction)Engine_track_state, METH_VARARGS,
-     "track_state(states, obstacles, target, step_num, terminates): the tensors a step must not "
-     "write while shared"},
+     "track_state(states, obstacles, target, step_num, terminates, states_alt|None): the tensors a "
+     "step must not write while shared"},
     {"shared_state", (PyCFunction)Engine_shared_state, METH_NOARGS,
-     "(states_shared, obstacles_shared, target_shared)"},
+     "(states, obstacles, target, step_num, terminates, states_alt) shared flags"},
+    {"states", (PyCFunction)Engine_states, METH_NOARGS, "the current states tensor"},
+    {"states_alt", (PyCFunction)Engine_states_alt, METH_NOARGS,
+     "the buffer the next step writes the states into, or None"},
     {"last_finished", (PyCFunction)Engine_last_finished, METH_NOARGS,
      "(terminated, truncated) of the last step or None"},
     {"pool_info", (PyCFunction)Engine_pool_info, METH_NOARGS, "[(obs_ptr, free)] per pooled set"},

@@ -54,7 +54,7 @@ __device__ __forceinline__ T in_sgpr(T p)
 // loop-invariant to the compiler, so a multi-tile loop keeps no per-pointer
 // induction variables or hoisted copies alive across tiles.
 struct StepPtrs {
-    float *states, *obstacles, *target, *step_num, *obs, *reward;
+    float *states, *states_out, *obstacles, *target, *step_num, *obs, *reward;
     uint8_t *terminates, *terminated, *truncated;
     const float *actions, *formation;
 };
@@ -63,6 +63,7 @@ __device__ __forceinline__ StepPtrs load_ptrs(KArgsK *K)
 {
     StepPtrs q;
     q.states = K->a.b.states;
+    q.states_out = K->a.b.states_out;  // = states unless double-buffered (marlnav_step)
     q.obstacles = K->a.b.obstacles;
     q.target = K->a.b.target;
     q.step_num = K->a.b.step_num;
@@ -101,7 +102,7 @@ __device__ __forceinline__ MarlnavParams load_params(KArgsK *K)
 // global -> LDS copy of NB bytes (multiple of 4) by LDS-DMA: 16 bytes per lane
 // per instruction, then single dwords. src (16-byte aligned) and dst are
 // wave-uniform.
-template <int NB>
+template <int NB, int AUX = 0>
 __device__ __forceinline__ void glds_span(const void *src, float *dst, unsigned lane)
 {
     constexpr int N16 = NB / 16, R4 = (NB % 16) / 4;
@@ -110,13 +111,13 @@ __device__ __forceinline__ void glds_span(const void *src, float *dst, unsigned 
         const char *s = in_sgpr(reinterpret_cast<const char *>(src) + k * 1024);
         if ((k + 1) * 64 <= N16 || (int)lane < N16 - k * 64)
             __builtin_amdgcn_global_load_lds(s + lane * 16u, (LdsVoid *)(dst + k * 256), 16, 0,
-                                             0);
+                                             AUX);
     }
     if constexpr (R4 > 0) {
         const char *s = in_sgpr(reinterpret_cast<const char *>(src) + N16 * 16);
         if ((int)lane < R4)
             __builtin_amdgcn_global_load_lds(s + lane * 4u, (LdsVoid *)(dst + N16 * 4), 4, 0,
-                                             0);
+                                             AUX);
     }
 }
 

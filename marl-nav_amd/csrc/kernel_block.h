@@ -39,11 +39,11 @@ struct BlockPlan {
 
 // Copy NB bytes of the block's span k into LDS by LDS-DMA from the wave
 // k % A (spans spread over the block's waves).
-template <int NB>
+template <int NB, int AUX = 0>
 __device__ __forceinline__ void block_glds(int k, int A, int w, const void *src, float *dst,
                                            unsigned lane)
 {
-    if (k % A == w) glds_span<NB>(src, dst, lane);
+    if (k % A == w) glds_span<NB, AUX>(src, dst, lane);
 }
 
 // plain strided copy of n elements by the block's NT threads (partial block)
@@ -387,9 +387,6 @@ __global__ void __launch_bounds__(64 * A)
                 wave_sync();  // every lane of this wave sees its list
                 reinit_reobs_native<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, wlist,
                                           (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
-                if (MARLNAV_AB & 8)
-                    reinit_reobs_native<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, wlist,
-                                              (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
             }
         }
         __syncthreads();
@@ -408,19 +405,15 @@ __global__ void __launch_bounds__(64 * A)
     }
     STAMP(5);
     if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
-        if (MARLNAV_AB & 4096)
-            block_store2<E * A * D, 4, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)), st, tid, wt);
-        else if (MARLNAV_AB & 8192)
-            block_store2<4, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)), st, tid, wt);
-        else if (!(MARLNAV_AB & 2))
-        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
+        if (!(MARLNAV_AB & 2))
+        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)),
                                                st, tid, wt);  // (E = 64: whole 16-byte pieces)
     } else if (!OBS_ONLY && full && NT % D == 0) {
         // ---- the same with the fused ObsNormalizer (utils.py:519-532):
         // thread tid only ever meets feature tid % D (NT is a multiple of D),
         // so its mean and scale are loaded once; every LDS read and every
         // division is issued ahead of the stores
-        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states + e0 * (A * 5)),
+        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)),
                                                st, tid, wt);
         KArgsK *kl = kargs_late<kHotKargsOff>();
         const int kk = tid % D;
@@ -460,7 +453,7 @@ __global__ void __launch_bounds__(64 * A)
                 gn[i] = (obs_rows[i] - ms[kk]) / ms[D + kk];
             }
         }
-        block_store(in_sgpr(b.states + e0 * (A * 5)), st, nrow * 5, tid, NT, wt);
+        block_store(in_sgpr(b.states_out + e0 * (A * 5)), st, nrow * 5, tid, NT, wt);
     }
     STAMP(6);
 #if MARLNAV_STAMPS

@@ -92,6 +92,51 @@ constexpr bool kSplitSpread = A * (1 + O + (A - 1)) >= 32;
 template <int A, int O>
 constexpr bool kSplitTpl = kSplitSpread<A, O> && O > 8;
 
+// Extra LDS cycles of the workgroup-spread row-reward read (kernel_split.h,
+// wave 0, lane = tile cw * R + row rw, reading the row's K bond terms at
+// tile base cw * F + BOND, row stride K, one ds_read_b32 per term): banks are
+// (dword address) mod 32, lanes conflict within each 32-lane half
+// (MI355X_MICROARCH.md §LDS). Round 2 left F = 40 mod 64 at A16/O32, a 2-way
+// conflict on every such read (+30 cycles per workgroup and step, the whole
+// rise of SQ_LDS_BANK_CONFLICT that round: 131k -> 166k per launch).
+__host__ __device__ constexpr int split_bond_conflicts(int BOND, int F, int K, int R)
+{
+    int extra = 0;
+    const int tiles = 64 / R < kWavesPerBlock ? 64 / R : kWavesPerBlock;
+    for (int j = 0; j < K; ++j)
+        for (int half = 0; half < 2; ++half) {
+            int worst = 1;
+            for (int bank = 0; bank < 32; ++bank) {
+                int n = 0;
+                for (int l = 32 * half; l < 32 * half + 32; ++l) {
+                    const int cw = l / R, rw = l % R;
+                    if (cw >= tiles) continue;
+                    const int a = cw * F + BOND + K * rw + j;
+                    n += (a % 32 == bank) ? 1 : 0;
+                }
+                worst = n > worst ? n : worst;
+            }
+            extra += worst - 1;
+        }
+    return extra;
+}
+
+// the smallest tile padding (floats, multiple of 4) with the fewest such
+// conflicts
+__host__ __device__ constexpr int split_tile_pad(int BOND, int F0, int K, int R)
+{
+    if (K <= 0) return 0;
+    int best = 0, best_c = split_bond_conflicts(BOND, F0, K, R);
+    for (int pad = 4; pad < 64 && best_c > 0; pad += 4) {
+        const int c = split_bond_conflicts(BOND, F0 + pad, K, R);
+        if (c < best_c) {
+            best_c = c;
+            best = pad;
+        }
+    }
+    return best;
+}
+
 template <int A, int O, int LPR>
 struct SplitPlan {
     static constexpr int EPW = 64 / LPR / A;  // envs per wave
@@ -108,7 +153,10 @@ struct SplitPlan {
     static constexpr int OBS = (SN + EPW + 3) & ~3;        // (R, DP)
     static constexpr int BOND = (OBS + R * DP + 3) & ~3;   // (R, A-1)
     static constexpr int RED = (BOND + R * (A - 1) + 3) & ~3;  // (R, 4)
-    static constexpr int FLOATS = RED + 4 * R;
+    // wave-tile stride, padded so that wave 0's one-lane-per-row read of
+    // every tile's bond terms (row_reward, after the workgroup barrier) is
+    // free of LDS bank conflicts (split_tile_pad)
+    static constexpr int FLOATS = RED + 4 * R + split_tile_pad(BOND, RED + 4 * R, A - 1, R);
     // formation (5A + 2 floats) and its observation template (2A^2 floats),
     // staged for the spread re-init of kSplitTpl shapes
     static constexpr int NF = 5 * A + 2, NCP = NF + 2 * A * A;
@@ -786,7 +834,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             }
     }
     if (!OBS_ONLY) {
-        float *gst = in_sgpr(b.states + e0 * (A * 5));
+        float *gst = in_sgpr(b.states_out + e0 * (A * 5));
         const int n = nr * 5;
         constexpr int SAL = gcd_c(R * 20, 16);
         if (SAL % 16 == 0 && ne == EPW) {

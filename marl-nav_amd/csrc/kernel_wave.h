@@ -218,7 +218,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                 b.obs_norm[(e0 * A + lane) * D + k] =
                     (out_row[k] - b.norm_mean[k]) / b.norm_scale[k];
         if (!OBS_ONLY)
-            wave_store(b.states + e0 * A * 5, st, nr * 5, lane, nullptr, nullptr, nullptr, 1, wt);
+            wave_store((b.states_out ? b.states_out : b.states) + e0 * A * 5, st, nr * 5, lane,
+                       nullptr, nullptr, nullptr, 1, wt);
         STAMP(6);
     }
     if (!OBS_ONLY && b.counters && lane == 0) {

@@ -498,6 +498,14 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
     StepArgs args = make_args(d, L);
     args.b = *b;
     args.step_idx = step_idx;
+    if (!args.b.states_out) {
+        args.b.states_out = args.b.states;  // in place
+    } else if (args.b.states_out != args.b.states) {
+        const size_t n = (size_t)d->num_parallel * d->num_agents * 5 * sizeof(float);
+        const char *a0 = (const char *)args.b.states, *b0 = (const char *)args.b.states_out;
+        if (a0 < b0 + n && b0 < a0 + n)
+            return fail(MARLNAV_EINVAL, "states_out overlaps states");
+    }
     const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
     const bool fsplit = g_family.load(std::memory_order_relaxed) == MARLNAV_FAMILY_SPLIT;
     if (family_allowed(MARLNAV_FAMILY_SPLIT))

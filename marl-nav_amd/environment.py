@@ -159,6 +159,8 @@ class Env(object):
         self._rng = rng if is_triangle else 'reference'
         self._mock_alias = init_p.get('init_method') == 'mock_init'
         self._env_offset = int(params.get('env_offset', 0))
+        # double-buffered states; False: updated in place
+        object.__setattr__(self, '_double_buffer', bool(params.get('states_double_buffer', True)))
         seed = params.get('seed', init_p.get('seed'))
         if seed is None:
             # native mode only: the reference-RNG path must not touch the torch
@@ -251,8 +253,19 @@ class Env(object):
         eng = self.__dict__.get('_engine')
         if eng is None:
             return
+        st = self._states
+        # the second states buffer (double-buffered states):
+        # the engine's, unless replaced or of another shape
+        alt = self.__dict__.pop('_states_alt_new', None)
+        if alt is None:
+            alt = eng.states_alt()
+        if alt is None or alt.shape != st.shape or alt.device != st.device:
+            alt = torch.empty_like(st)
+        if not self.__dict__.get('_double_buffer', True):
+            alt = None   # params['states_double_buffer'] = False: in place
         b = abi.MarlnavStepBuffers()
-        b.states = self._states.data_ptr()
+        b.states = st.data_ptr()
+        b.states_out = alt.data_ptr() if alt is not None else None
         b.obstacles = self._obstacles.data_ptr()
         b.target = self._target.data_ptr()
         b.step_num = self.__dict__['_step_num_t'].data_ptr()
@@ -267,8 +280,12 @@ class Env(object):
         fast = (not self._params_dirty and self._rng == 'native'
                 and self._init_sampler is self._default_init_sampler)
         eng.configure(bytes(self._dims), bytes(self._cparams), bytes(b), fast)
-        eng.track_state(self._states, self._obstacles, self._target,
-                        self.__dict__['_step_num_t'], self.__dict__['_terminates_t'])
+        eng.track_state(st, self._obstacles, self._target,
+                        self.__dict__['_step_num_t'], self.__dict__['_terminates_t'], alt)
+        # from here the engine holds the state buffers: Env.states asks it for
+        # the current one (the two swap roles every step)
+        self.__dict__['_states_t'] = None
+        del st, alt
 
     def _unshare_state(self):
         """Copy-on-write of the tensors a step writes in place. The
@@ -277,15 +294,22 @@ class Env(object):
         :219, so a caller still holding one from before a step keeps its
         values - for `states` the moved ones, since `_move_agents` writes it
         in place first (:113-123), and for `_step_num` the incremented ones
-        (:96, in place). The kernel writes all five in place; when the engine
-        reports one referenced outside the Env, the Env moves to a copy
-        (stream-ordered) before the step. Returns (held pre-step `states` or
+        (:96, in place). The kernel writes obstacles, target, step_num and
+        terminates in place and the new states into the second states buffer;
+        when the engine reports one of them referenced outside the Env, the
+        Env moves to a copy (stream-ordered) before the step, and a held
+        second states buffer is replaced. Returns (held pre-step `states` or
         None, held pre-step `_step_num` or None) for `_finish_held`."""
         shared = self._engine.shared_state()
         held = held_sn = None
         if shared[0]:
+            # the step reads the current buffer and writes the other one, so
+            # the holder's tensor keeps its pre-step values until _finish_held
+            # moves it; after the step it is the second buffer, which is held
+            # and so replaced before the next step (shared[5])
             held = self._states
-            object.__setattr__(self, '_states', held.clone())
+        if shared[5]:
+            self.__dict__['_states_alt_new'] = torch.empty_like(self._states)
         if shared[1]:
             object.__setattr__(self, '_obstacles', self._obstacles.clone())
         if shared[2]:
@@ -428,6 +452,20 @@ class Env(object):
         return o
 
     # ------------------------------------------------------------ state API
+    @property
+    def _states(self):
+        """The current states buffer: the engine's once it holds the state
+        buffers (_configure), which swap roles every step (double-buffered
+        states: the kernel reads one and writes the other)."""
+        t = self.__dict__.get('_states_t')
+        if t is not None:
+            return t
+        return self.__dict__['_engine'].states()
+
+    @_states.setter
+    def _states(self, t):
+        self.__dict__['_states_t'] = t   # handed to the engine by _configure
+
     @property
     def states(self):
         return self._states

@@ -28,6 +28,8 @@ def main():
                 args = pkg.default_args(num_parallel=P, num_agents=A, num_obstacles=O)
                 params = pkg.set_env_params(args, dev)
                 params.update(rng="native", seed=20251003, _lib=h)
+                if os.path.basename(p) in os.environ.get("INPLACE", "").split(","):
+                    params["states_double_buffer"] = False
                 env = pkg.Env(params)
                 if warm is None:  # clock ramp once per config
                     bench.prewarm(env, acts, 0.3)

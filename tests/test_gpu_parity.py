@@ -360,19 +360,22 @@ def test_held_state_tensors_see_what_the_reference_shows(pkg):
     rebinds them, environment.py:79-81): a caller holding the pre-step tensor,
     or a view of it, keeps its values here too. A held `states` receives the
     moved states (the reference moves in place, :113-123) but not the re-init
-    (:79 rebinds). Nothing held: the step writes the Env's buffers in place (no
-    copies). Holders change nothing else: the trajectory equals one run
-    without holders, bit for bit."""
+    (:79 rebinds). Nothing held: no copies - obstacles and target are written
+    in place, the states alternate between the Env's two state buffers (the
+    step reads one and writes the other). Holders change nothing else: the
+    trajectory equals one run without holders, bit for bit."""
     P = 4096 + 7
     env = make_env(pkg, P, 3, 3, episode_len=3)   # every env truncates at step 3
     twin = make_env(pkg, P, 3, 3, episode_len=3)
     acts = [torch.rand(P, 3, 2, device=DEV) - 0.5 for _ in range(3)]
-    p_st, p_ob, p_tg = env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()
+    p_ob, p_tg = env.obstacles.data_ptr(), env.target.data_ptr()
+    st_ptrs = set()
     for k in range(4):
         env.step(acts[k % 3])
         twin.step(acts[k % 3])
-    assert (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()) == \
-        (p_st, p_ob, p_tg)
+        st_ptrs.add(env.states.data_ptr())
+    assert (env.obstacles.data_ptr(), env.target.data_ptr()) == (p_ob, p_tg)
+    assert len(st_ptrs) == 2   # double-buffered states, no allocation
     ob, tg_view = env.obstacles, env.target[:, 0]
     ob0, tg0 = ob.clone(), tg_view.clone()
     for k in range(4, 8):
@@ -402,10 +405,13 @@ def test_held_state_tensors_see_what_the_reference_shows(pkg):
         assert torch.equal(a, b)
     # holders gone (the loop's names too): back to in-place steps
     del ob, tg_view, a, b
-    q = (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr())
-    for k in range(3):
-        env.step(acts[k])
-    assert (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()) == q
+    env.step(acts[0])   # (replaces the second states buffer the holder had)
+    q = (env.obstacles.data_ptr(), env.target.data_ptr())
+    st_ptrs = set()
+    for k in range(4):
+        env.step(acts[k % 3])
+        st_ptrs.add(env.states.data_ptr())
+    assert (env.obstacles.data_ptr(), env.target.data_ptr()) == q and len(st_ptrs) == 2
 
 
 def test_held_states_reference_rng_mode(pkg):

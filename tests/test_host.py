@@ -104,45 +104,53 @@ def test_engine_fast_path_falls_back_for_other_actions():
 
 
 def test_engine_reports_held_state_tensors():
-    """Copy-on-write rule for states / obstacles / target / step_num /
-    terminates (environment.py:79-83 and :219 rebind them): a
-    tracked tensor counts as held once anything beyond its owner's attribute
-    and the engine refers to it, or a view shares its storage; a held tensor
-    keeps steps off the fast path."""
+    """Copy-on-write rule for the tensors a step writes (environment.py:79-83
+    and :219 rebind them): obstacles / target / step_num /
+    terminates count as held once anything beyond their owner's attribute and
+    the engine refers to them, the two state buffers (which only the engine
+    holds: Env.states asks it) once anything at all does; a view sharing the
+    storage counts too; a held tensor keeps steps off the fast path."""
     calls = []
     eng, cb = _cpu_engine(calls)
 
     class Owner:
         pass
     o = Owner()
-    o.s, o.ob, o.tg = torch.zeros(10, 3, 5), torch.zeros(10, 3, 2), torch.zeros(10, 1, 2)
+    o.ob, o.tg = torch.zeros(10, 3, 2), torch.zeros(10, 1, 2)
     o.sn, o.tm = torch.zeros(10), torch.zeros(10, dtype=torch.bool)
-    track = lambda: eng.track_state(o.s, o.ob, o.tg, o.sn, o.tm)  # noqa: E731
-    none = (False,) * 5
-    track()
+    track = lambda s, alt: eng.track_state(s, o.ob, o.tg, o.sn, o.tm, alt)  # noqa: E731
+    none = (False,) * 6
+    track(torch.zeros(10, 3, 5), torch.zeros(10, 3, 5))
     assert eng.shared_state() == none
-    s = o.s
-    assert eng.shared_state() == (True, False, False, False, False)
+    s = eng.states()
+    assert eng.shared_state() == (True, False, False, False, False, False)
     del s
+    a = eng.states_alt()[2:]
+    assert eng.shared_state() == (False, False, False, False, False, True)
+    del a
     v = o.tg[:, 0]
-    assert eng.shared_state() == (False, False, True, False, False)
+    assert eng.shared_state() == (False, False, True, False, False, False)
     del v
     lst = [o.ob]
-    assert eng.shared_state() == (False, True, False, False, False)
+    assert eng.shared_state() == (False, True, False, False, False, False)
     del lst
     sn = o.sn
-    assert eng.shared_state() == (False, False, False, True, False)
+    assert eng.shared_state() == (False, False, False, True, False, False)
     del sn
     tm = o.tm[3:]
-    assert eng.shared_state() == (False, False, False, False, True)
+    assert eng.shared_state() == (False, False, False, False, True, False)
     del tm
     assert eng.shared_state() == none
-    # re-tracking releases the old tensors
-    old = o.s
-    o.s = o.s.clone()
-    track()
-    assert eng.shared_state() == none
-    del old
+    # a launch swaps the state buffers: the one written becomes current
+    cur, alt = eng.states().data_ptr(), eng.states_alt().data_ptr()
+    eng.launch(0, None, 0)
+    assert (eng.states().data_ptr(), eng.states_alt().data_ptr()) == (alt, cur)
+    # re-tracking releases the old tensors; no second buffer: in place
+    track(torch.zeros(10, 3, 5), None)
+    assert eng.shared_state() == none and eng.states_alt() is None
+    p0 = eng.states().data_ptr()
+    eng.launch(0, None, 0)
+    assert eng.states().data_ptr() == p0
 
 
 def test_dlpack_export_counts_as_a_holder():
@@ -169,13 +177,17 @@ def test_dlpack_export_counts_as_a_holder():
     class Owner:
         pass
     o = Owner()
-    o.s, o.ob, o.tg = torch.zeros(10, 3, 5), torch.zeros(10, 3, 2), torch.zeros(10, 1, 2)
+    o.ob, o.tg = torch.zeros(10, 3, 2), torch.zeros(10, 1, 2)
     o.sn, o.tm = torch.zeros(10), torch.zeros(10, dtype=torch.bool)
-    eng.track_state(o.s, o.ob, o.tg, o.sn, o.tm)
-    cap = to_dlpack(o.s)
+    eng.track_state(torch.zeros(10, 3, 5), o.ob, o.tg, o.sn, o.tm, torch.zeros(10, 3, 5))
+    cap = to_dlpack(eng.states())
     assert eng.shared_state()[0]
     del cap
     assert not eng.shared_state()[0]
+    cap = to_dlpack(o.ob)
+    assert eng.shared_state()[1]
+    del cap
+    assert not any(eng.shared_state())
 
 
 def test_cli_mirrors_reference_arguments():
