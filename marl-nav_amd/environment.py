@@ -159,8 +159,10 @@ class Env(object):
         self._rng = rng if is_triangle else 'reference'
         self._mock_alias = init_p.get('init_method') == 'mock_init'
         self._env_offset = int(params.get('env_offset', 0))
-        # double-buffered states; False: updated in place
-        object.__setattr__(self, '_double_buffer', bool(params.get('states_double_buffer', True)))
+        # params['states_double_buffer']: the step reads one state buffer and
+        # writes the other (MarlnavStepBuffers.states_out), the two swapping
+        # roles every step; default in place (measured no faster)
+        object.__setattr__(self, '_double_buffer', bool(params.get('states_double_buffer', False)))
         seed = params.get('seed', init_p.get('seed'))
         if seed is None:
             # native mode only: the reference-RNG path must not touch the torch
@@ -261,8 +263,8 @@ class Env(object):
             alt = eng.states_alt()
         if alt is None or alt.shape != st.shape or alt.device != st.device:
             alt = torch.empty_like(st)
-        if not self.__dict__.get('_double_buffer', True):
-            alt = None   # params['states_double_buffer'] = False: in place
+        if not self.__dict__.get('_double_buffer', False):
+            alt = None   # in place (the default)
         b = abi.MarlnavStepBuffers()
         b.states = st.data_ptr()
         b.states_out = alt.data_ptr() if alt is not None else None
@@ -303,11 +305,15 @@ class Env(object):
         shared = self._engine.shared_state()
         held = held_sn = None
         if shared[0]:
-            # the step reads the current buffer and writes the other one, so
-            # the holder's tensor keeps its pre-step values until _finish_held
-            # moves it; after the step it is the second buffer, which is held
-            # and so replaced before the next step (shared[5])
             held = self._states
+            if not self.__dict__.get('_double_buffer', False):
+                # in place: the Env steps a copy
+                object.__setattr__(self, '_states', held.clone())
+            # double-buffered, the step reads the current buffer and writes
+            # the other one, so the holder's tensor keeps its pre-step values
+            # until _finish_held moves it; after the step it is the second
+            # buffer, which is held and so replaced before the next step
+            # (shared[5])
         if shared[5]:
             self.__dict__['_states_alt_new'] = torch.empty_like(self._states)
         if shared[1]:

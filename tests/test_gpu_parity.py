@@ -360,22 +360,19 @@ def test_held_state_tensors_see_what_the_reference_shows(pkg):
     rebinds them, environment.py:79-81): a caller holding the pre-step tensor,
     or a view of it, keeps its values here too. A held `states` receives the
     moved states (the reference moves in place, :113-123) but not the re-init
-    (:79 rebinds). Nothing held: no copies - obstacles and target are written
-    in place, the states alternate between the Env's two state buffers (the
-    step reads one and writes the other). Holders change nothing else: the
-    trajectory equals one run without holders, bit for bit."""
+    (:79 rebinds). Nothing held: the step writes the Env's buffers in place (no
+    copies). Holders change nothing else: the trajectory equals one run
+    without holders, bit for bit."""
     P = 4096 + 7
     env = make_env(pkg, P, 3, 3, episode_len=3)   # every env truncates at step 3
     twin = make_env(pkg, P, 3, 3, episode_len=3)
     acts = [torch.rand(P, 3, 2, device=DEV) - 0.5 for _ in range(3)]
-    p_ob, p_tg = env.obstacles.data_ptr(), env.target.data_ptr()
-    st_ptrs = set()
+    p_st, p_ob, p_tg = env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()
     for k in range(4):
         env.step(acts[k % 3])
         twin.step(acts[k % 3])
-        st_ptrs.add(env.states.data_ptr())
-    assert (env.obstacles.data_ptr(), env.target.data_ptr()) == (p_ob, p_tg)
-    assert len(st_ptrs) == 2   # double-buffered states, no allocation
+    assert (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()) == \
+        (p_st, p_ob, p_tg)
     ob, tg_view = env.obstacles, env.target[:, 0]
     ob0, tg0 = ob.clone(), tg_view.clone()
     for k in range(4, 8):
@@ -405,13 +402,10 @@ def test_held_state_tensors_see_what_the_reference_shows(pkg):
         assert torch.equal(a, b)
     # holders gone (the loop's names too): back to in-place steps
     del ob, tg_view, a, b
-    env.step(acts[0])   # (replaces the second states buffer the holder had)
-    q = (env.obstacles.data_ptr(), env.target.data_ptr())
-    st_ptrs = set()
-    for k in range(4):
-        env.step(acts[k % 3])
-        st_ptrs.add(env.states.data_ptr())
-    assert (env.obstacles.data_ptr(), env.target.data_ptr()) == q and len(st_ptrs) == 2
+    q = (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr())
+    for k in range(3):
+        env.step(acts[k])
+    assert (env.states.data_ptr(), env.obstacles.data_ptr(), env.target.data_ptr()) == q
 
 
 def test_held_states_reference_rng_mode(pkg):
@@ -431,6 +425,43 @@ def test_held_states_reference_rng_mode(pkg):
     torch.cuda.synchronize()
     assert torch.equal(held, mv.states)
     assert not torch.equal(held, env.states)
+
+
+@pytest.mark.parametrize("P,A,O", [(4096 + 5, 3, 3), (60, 16, 32), (333, 5, 2)])
+def test_double_buffered_states(pkg, P, A, O):
+    """params['states_double_buffer'] (MarlnavStepBuffers.states_out): the
+    step reads one state buffer and writes the other, the two alternating
+    with no allocation; every output and state bit-identical to the in-place
+    Env, a held `states` still sees what the reference shows (the moved
+    states), and the buffer it holds is replaced, not written, afterwards."""
+    env = make_env(pkg, P, A, O, episode_len=4)
+    params = dict(env.params, states_double_buffer=True)
+    db2 = pkg.Env(params)
+    acts = [torch.rand(P, A, 2, device=DEV) - 0.5 for _ in range(3)]
+    ptrs = set()
+    for k in range(9):
+        o1, r1, te1, tr1 = env.step(acts[k % 3])
+        o2, r2, te2, tr2 = db2.step(acts[k % 3])
+        ptrs.add(db2.states.data_ptr())
+        assert torch.equal(o1._packed, o2._packed) and torch.equal(r1, r2)
+        assert torch.equal(te1, te2) and torch.equal(tr1, tr2)
+        assert torch.equal(env.states, db2.states)
+        if k == 5:
+            held, held0 = db2.states, db2.states.clone()
+            ob_k, tg_k = db2.obstacles.clone(), db2.target.clone()
+        if k == 6:
+            mv = make_env(pkg, P, A, O, episode_len=10 ** 9)
+            mv._ob_coll_dist = mv._ag_coll_dist = float("-inf")
+            mv.states, mv.obstacles, mv.target = held0, ob_k, tg_k
+            mv.step(acts[k % 3])
+            torch.cuda.synchronize()
+            assert torch.equal(held, mv.states)
+            moved = held.clone()
+            del mv
+        if k == 8:
+            torch.cuda.synchronize()
+            assert torch.equal(held, moved)   # not written by later steps
+    assert len(ptrs) >= 2 and all(p != held.data_ptr() for p in [db2.states.data_ptr()])
 
 
 def test_held_states_pair_split_kernel(pkg):
