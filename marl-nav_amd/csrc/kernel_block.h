@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(64 * A)
                     uint64_t *cnt = kl->a.b.counters;
                     const int64_t slots = kl->a.waves;
                     if (cnt) {
-                        const int64_t sl = blk % slots;
+                        const int64_t sl = blk < slots ? blk : blk % slots;
                         if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
                         if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + sl], (unsigned long long)c_col);
                         if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
