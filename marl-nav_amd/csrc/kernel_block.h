@@ -261,7 +261,12 @@ __global__ void __launch_bounds__(64 * A)
         float rowv[D];
         RowOut ro;
         bool unused = true;
-        if (__builtin_expect(fast, 1))
+        if (__builtin_expect(fast, 1) && !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f &&
+            pr.max_at_prop_d == 2.0f)
+            ro = observe_row_own<A, O, !OBS_ONLY, true, true>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
+                                                              lds + BP::TG + 2 * l, w, ox, oy, dx,
+                                                              dy, rowv, pr, unused);
+        else if (__builtin_expect(fast, 1))
             ro = observe_row_own<A, O, !OBS_ONLY, true>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
                                                         lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
                                                         rowv, pr, unused);
@@ -304,15 +309,15 @@ __global__ void __launch_bounds__(64 * A)
 #pragma unroll
                 for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
-                out_el(b.reward, e, rsum / (float)A, wt);              // torch.mean (:233)
+                out_el(b.reward, e, rsum / (float)A);              // torch.mean (:233)
 
                 float step_num = lds[BP::SN + l] + 1.0f;           // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
                 const bool terminated = any_col || term_old;       // :213-214
-                out_el(b.terminates, e, (uint8_t)(!term_old && all_in), wt);  // :218-219
-                out_el(b.terminated, e, (uint8_t)terminated, wt);
-                out_el(b.truncated, e, (uint8_t)truncated, wt);
+                out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
+                out_el(b.terminated, e, (uint8_t)terminated);
+                out_el(b.truncated, e, (uint8_t)truncated);
                 fin = truncated || terminated;                     // :102-104
                 if (NOISY && fin) {  // noisy native re-init: serial per env
                     KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -333,12 +338,12 @@ __global__ void __launch_bounds__(64 * A)
                                                 (uint64_t)(kl->a.env_offset + e), kl->a.step_idx,
                                                 st + 5 * A * l, obl, tgl);
                         float *gob = kl->a.b.obstacles;
-                        for (int i = 0; i < 2 * O; ++i) out_el(gob, e * O * 2 + i, obl[i], wt);
-                        out_el(kl->a.b.target, 2 * e, tgl[0], wt);
-                        out_el(kl->a.b.target, 2 * e + 1, tgl[1], wt);
+                        for (int i = 0; i < 2 * O; ++i) out_el(gob, e * O * 2 + i, obl[i]);
+                        out_el(kl->a.b.target, 2 * e, tgl[0]);
+                        out_el(kl->a.b.target, 2 * e + 1, tgl[1]);
                     }
                 }
-                out_el(b.step_num, e, fin ? blend_in(step_num, 0.0f) : step_num, wt);
+                out_el(b.step_num, e, fin ? blend_in(step_num, 0.0f) : step_num);
                 tr_l = truncated;
                 co_l = any_col;
                 ta_l = all_in;
@@ -447,10 +452,15 @@ __global__ void __launch_bounds__(64 * A)
             }
             __syncthreads();
             float *gn = kl->a.b.obs_norm + e0 * (A * D);
+            const OutBuf nb = out_buf(gn, 4u * nrow * D);
 #pragma unroll 4
             for (int i = tid; i < nrow * D; i += NT) {
                 const int kk = i % D;
-                gn[i] = (obs_rows[i] - ms[kk]) / ms[D + kk];
+                const float v = (obs_rows[i] - ms[kk]) / ms[D + kk];
+                if (kWtOut && wt)
+                    wt_st(nb, 4u * i, v);
+                else
+                    gn[i] = v;
             }
         }
         block_store(in_sgpr(b.states_out + e0 * (A * 5)), st, nrow * 5, tid, NT, wt);

@@ -169,7 +169,6 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
 {
     float *gob = kl->a.b.obstacles;
     float *gtg = kl->a.b.target;
-    const bool wt = (kl->p.flags & kWriteThroughFlag) != 0;
     const float *fs = kl->a.b.fresh_states;
     if (fs) {
         const float *fo = kl->a.b.fresh_obstacles, *ft = kl->a.b.fresh_target;
@@ -187,13 +186,13 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
                 float *d = ev.obst(c) + j;
                 const float v = blend_in(*d, fo[e * O * 2 + j]);
                 *d = v;
-                out_el(gob, e * O * 2 + j, v, wt);
+                out_el(gob, e * O * 2 + j, v);
             } else {
                 const int j = kk - 5 * A - 2 * O;
                 float *d = ev.targ(c) + j;
                 const float v = blend_in(*d, ft[2 * e + j]);
                 *d = v;
-                out_el(gtg, 2 * e + j, v, wt);
+                out_el(gtg, 2 * e + j, v);
             }
         }
         return;
@@ -218,7 +217,7 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
             float *d = ev.targ(c) + j;
             const float v = blend_in(*d, form[kk]);
             *d = v;
-            out_el(gtg, 2 * e + j, v, wt);
+            out_el(gtg, 2 * e + j, v);
             if (unclean && __float_as_uint(v) != __float_as_uint(form[kk])) *unclean = 1;
         } else {
             const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
@@ -231,13 +230,13 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
             const int64_t g = e * O * 2 + 2 * j;
             o[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
             o[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
-            out_el(gob, g, o[0], wt);
-            out_el(gob, g + 1, o[1], wt);
+            out_el(gob, g, o[0]);
+            out_el(gob, g + 1, o[1]);
             if (j + 1 < O) {
                 o[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
                 o[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
-                out_el(gob, g + 2, o[2], wt);
-                out_el(gob, g + 3, o[3], wt);
+                out_el(gob, g + 2, o[2]);
+                out_el(gob, g + 3, o[3]);
             }
         }
     }
@@ -264,7 +263,6 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
     const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
     float *gob = kl->a.b.obstacles;
     float *gtg = kl->a.b.target;
-    const bool wt = (kl->p.flags & kWriteThroughFlag) != 0;
     const int n = nfin * NI;
     for (int base = 0; base < n; base += nt) {
         const int i = base + tid;
@@ -352,20 +350,20 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
                 float *d = ev.targ(c) + j;
                 const float v = blend_in(*d, form[k2]);
                 *d = v;
-                out_el(gtg, 2 * e + j, v, wt);
+                out_el(gtg, 2 * e + j, v);
             } else {
                 const int j = 2 * jb;
                 float *o = ev.obst(c) + 2 * j;
                 const int64_t g = e * O * 2 + 2 * j;
                 o[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
                 o[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
-                out_el(gob, g, o[0], wt);
-                out_el(gob, g + 1, o[1], wt);
+                out_el(gob, g, o[0]);
+                out_el(gob, g + 1, o[1]);
                 if (j + 1 < O) {
                     o[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
                     o[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
-                    out_el(gob, g + 2, o[2], wt);
-                    out_el(gob, g + 3, o[3], wt);
+                    out_el(gob, g + 2, o[2]);
+                    out_el(gob, g + 3, o[3]);
                 }
             }
         }

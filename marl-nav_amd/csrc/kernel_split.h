@@ -573,14 +573,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 #pragma unroll
             for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
             const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
-            out_el(b.reward, e, rsum / (float)A, wt);             // torch.mean (:233)
+            out_el(b.reward, e, rsum / (float)A);             // torch.mean (:233)
             float step_num = sn_v + 1.0f;                      // :96
             const bool truncated = step_num > pr.trunc_after;  // :97
             const bool term_old = term_v != 0u;
             const bool terminated = any_col || term_old;       // :213-214
-            out_el(b.terminates, e, (uint8_t)(!term_old && all_in), wt);  // :218-219
-            out_el(b.terminated, e, (uint8_t)terminated, wt);
-            out_el(b.truncated, e, (uint8_t)truncated, wt);
+            out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
+            out_el(b.terminated, e, (uint8_t)terminated);
+            out_el(b.truncated, e, (uint8_t)truncated);
             const bool fin = truncated || terminated;          // :102-104
             if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
                 KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -610,12 +610,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                                             (uint64_t)(kl->a.env_offset + e), kl->a.step_idx, s5,
                                             obl, tgl);
                 }
-                for (int i = 0; i < 2 * O; ++i) out_el(gob, e * O * 2 + i, obl[i], wt);
-                out_el(gtg, 2 * e, tgl[0], wt);
-                out_el(gtg, 2 * e + 1, tgl[1], wt);
+                for (int i = 0; i < 2 * O; ++i) out_el(gob, e * O * 2 + i, obl[i]);
+                out_el(gtg, 2 * e, tgl[0]);
+                out_el(gtg, 2 * e + 1, tgl[1]);
             }
             if (fin) step_num = blend_in(step_num, 0.0f);
-            out_el(b.step_num, e, step_num, wt);
+            out_el(b.step_num, e, step_num);
             tr_l = truncated;
             co_l = any_col;
             ta_l = all_in;
@@ -659,6 +659,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                                          wlc + SP::BOND + rw * (A - 1));
                 }
                 wave_sync();
+                STAMPX(0);
                 const int ce = (int)lane;  // env code: wave ce / EPW, env ce % EPW
                 const int64_t e = blk0 * EPW + ce;
                 const bool on = ce < live * EPW && e < P;
@@ -678,8 +679,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 c_trunc = __popcll(__ballot(tr_l));
                 c_col = __popcll(__ballot(co_l));
                 c_tar = __popcll(__ballot(ta_l));
+                STAMPX(1);
             }
             __syncthreads();
+            STAMPX(2);
             const FlatFinList list{bslot, bcnt[0]};
 #if MARLNAV_STAMPS
             stamp_nfin = list.total();
@@ -713,6 +716,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     __syncthreads();
                     reinit_block<A, O>(kl, ev, ftp, list, nfin, tid, nt, unclean);
                     __syncthreads();
+                    STAMPX(3);
                     if (*unclean == 0)
                         reobs_block_tpl<A, O>(ev, list, nfin, pr.cap_distance,
                                               reinterpret_cast<const float2 *>(ftp + SP::NF),
@@ -826,12 +830,18 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     out_st<kNtRows>(gobs + i, src[i]);
             }
         }
-        if (gnorm)
+        if (gnorm) {
+            const OutBuf nb = out_buf(gnorm, 4u * n);
 #pragma unroll 8  // (mean/scale loads of 8 iterations in flight at once)
             for (int i = (int)lane; i < n; i += 64) {
                 const int rr = i / D, kk = i - rr * D;
-                out_el(gnorm, (int64_t)i, (src[rr * SP::DP + kk] - mean[kk]) / scale[kk], wt);
+                const float v = (src[rr * SP::DP + kk] - mean[kk]) / scale[kk];
+                if (kWtOut && wt)
+                    wt_st(nb, 4u * i, v);
+                else
+                    gnorm[i] = v;
             }
+        }
     }
     if (!OBS_ONLY) {
         float *gst = in_sgpr(b.states_out + e0 * (A * 5));

@@ -134,15 +134,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                 }
                 const float *rr = all_in ? rhit : rmiss;
                 const float rsum = torch_row_sum(rr + lane * A, A, [](float r) { return r; });
-                out_el(b.reward, e, rsum / (float)A, wt);                     // torch.mean (:233)
+                out_el(b.reward, e, rsum / (float)A);                     // torch.mean (:233)
 
                 float step_num = step_num_in + 1.0f;               // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = term_in != 0;
                 const bool terminated = any_col || term_old;       // :213-214
-                out_el(b.terminates, e, (uint8_t)(!term_old && all_in), wt);  // :218-219
-                out_el(b.terminated, e, (uint8_t)terminated, wt);
-                out_el(b.truncated, e, (uint8_t)truncated, wt);
+                out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
+                out_el(b.terminated, e, (uint8_t)terminated);
+                out_el(b.truncated, e, (uint8_t)truncated);
                 fin = truncated || terminated;                     // :102-104
                 if (fin) {
                     float *sts = st + 5 * A * lane;
@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) wave_kernel(StepArgs args
                     b.target[2 * e + 1] = tge[1];
                     step_num = blend_in(step_num, 0.0f);
                 }
-                out_el(b.step_num, e, step_num, wt);
+                out_el(b.step_num, e, step_num);
                 envbits[lane] = fin ? 1u : 0u;
                 tr_l = truncated;
                 co_l = any_col;

@@ -19,7 +19,15 @@ __device__ unsigned long long *g_stamps;
             sp_[2 * (k) + 1] = clock64();                                          \
         }                                                                          \
     } while (0)
+// extra realtime-only stamps at slots 20..23 (diagnostic sub-phases)
+#define STAMPX(k)                                                                  \
+    do {                                                                           \
+        if (lane == 0) g_stamps[(size_t)gw * 24 + 20 + (k)] = wall_clock64();      \
+    } while (0)
 #else
+#define STAMPX(k) \
+    do {          \
+    } while (0)
 #define STAMP(k) \
     do {         \
     } while (0)
@@ -29,4 +37,7 @@ __device__ unsigned long long *g_stamps;
 // ... -DMARLNAV_AB=bits); 0 in the product build.
 #ifndef MARLNAV_AB
 #define MARLNAV_AB 0
+#endif
+#ifndef MARLNAV_AB_NOREFC
+#define MARLNAV_AB_NOREFC 0
 #endif
