@@ -384,14 +384,17 @@ __global__ void __launch_bounds__(64 * A)
                       reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
             }
             const uint64_t fm = __ballot(fin);
+            STAMPX(0);
             if (fm && !(MARLNAV_AB & 1)) {
                 int *wlist = reinterpret_cast<int *>(lds + BP::LIST2) + E * (w - 1);
                 if (fin)
                     wlist[__builtin_amdgcn_mbcnt_hi(
                         (unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] = l;
                 wave_sync();  // every lane of this wave sees its list
+                STAMPX(1);
                 reinit_reobs_native<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, wlist,
                                           (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
+                STAMPX(2);
             }
         }
         __syncthreads();
@@ -470,10 +473,10 @@ __global__ void __launch_bounds__(64 * A)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     STAMP(7);
     if (lane == 0) {
-        g_stamps[(size_t)gw * 24 + 16] = t_entry;
-        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
-        g_stamps[(size_t)gw * 24 + 19] = OBS_ONLY ? 0u : (unsigned)reinterpret_cast<const int *>(lds + BP::FLG)[0];
+        *STAMP_PTR((size_t)gw * 24 + 16) = t_entry;
+        *STAMP_PTR((size_t)gw * 24 + 17) = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        *STAMP_PTR((size_t)gw * 24 + 18) = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+        *STAMP_PTR((size_t)gw * 24 + 19) = OBS_ONLY ? 0u : (unsigned)reinterpret_cast<const int *>(lds + BP::FLG)[0];
     }
 #endif
     (void)gw;

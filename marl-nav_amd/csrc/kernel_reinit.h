@@ -250,122 +250,167 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
 // env: A*(1+O+A-1) pairs (written into the packed rows), 5A+2 template
 // floats and ceil(O/2) Philox blocks (written to the LDS state and the
 // global obstacles/target).
+//
+// With two or more waves the items go by kind: the first half of the waves
+// takes the pair items, the rest the template / obstacle items, so no wave
+// runs both code paths one after the other (the pass is the tail of the
+// block: issue-bound on the few waves that have items). A wave with no item
+// left skips the pass. `tid` and `nt` are wave-aligned.
+template <int A, int O>
+struct NativeItems {
+    static constexpr int NP = 1 + O + (A - 1), NB = (O + 1) / 2;
+    static constexpr int NPAIR = A * NP, NREST = 5 * A + 2 + NB;
+};
+
+__device__ __forceinline__ void philox_obst_block(uint32_t cc[4], int jb, uint64_t gid, uint64_t sidx,
+                                                  uint64_t seed)
+{
+    cc[0] = (uint32_t)jb;
+    cc[1] = (uint32_t)sidx;
+    cc[2] = (uint32_t)gid;
+    cc[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
+    philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// pair item kk (< NPAIR) of finished env c; `on` false: computes, stores nothing
+template <int A, int O, class Envs>
+__device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, const float *form, int c,
+                                                 int kk, bool on, float cap)
+{
+    using IT = NativeItems<A, O>;
+    const int ag = kk / IT::NP, p = kk - ag * IT::NP;
+    uint32_t cc[4] = {0u, 0u, 0u, 0u};
+    if (p >= 1 && p <= O)  // obstacle p - 1: its Philox block
+        philox_obst_block(cc, (p - 1) >> 1, (uint64_t)(kl->a.env_offset + ev.env(c)), kl->a.step_idx,
+                          kl->p.seed);
+    // inputs: the blend of the env's current value (LDS; other items may be
+    // blending it in place meanwhile - blend_in is idempotent) with its fresh
+    // value (template or Philox draw)
+    const float *s = form + 5 * ag;
+    const float *so = ev.state(c) + 5 * ag;
+    const float ox = blend_in(so[0], s[0]), oy = blend_in(so[1], s[1]);
+    const float dx = blend_in(so[2], s[2]), dy = blend_in(so[3], s[3]);
+    float px, py;
+    int sa, sd;
+    if (p == 0) {            // target
+        px = blend_in(ev.targ(c)[0], form[5 * A]);
+        py = blend_in(ev.targ(c)[1], form[5 * A + 1]);
+        sa = 0;
+        sd = 1;
+    } else if (p <= O) {     // obstacle p - 1: components of its Philox block
+        const bool hi = ((p - 1) & 1) != 0;
+        const uint32_t ux = hi ? cc[2] : cc[0], uy = hi ? cc[3] : cc[1];
+        const float *oo = ev.obst(c) + 2 * (p - 1);
+        px = blend_in(oo[0], kl->p.obs_range_x * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + kl->p.obs_mean_x);
+        py = blend_in(oo[1], kl->p.obs_range_y * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + kl->p.obs_mean_y);
+        sa = 1 + p;
+        sd = 1 + O + p;
+    } else {                 // other agent kx, skipping self
+        const int kx = p - O - 1;
+        const int m = kx + (kx >= ag ? 1 : 0);
+        const float *q = form + 5 * m;
+        const float *qo = ev.state(c) + 5 * m;
+        px = blend_in(qo[0], q[0]);
+        py = blend_in(qo[1], q[1]);
+        sa = 2 + 2 * O + kx;
+        sd = 2 + 2 * O + (A - 1) + kx;
+    }
+    const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+    bool unused = true;
+    float d, ang;
+    if (__ballot(on && !cok) == 0ull) {
+        d = pair_dist<true>(ox, oy, px, py, unused);
+        ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+    } else {
+        d = pair_dist<false>(ox, oy, px, py, unused);
+        ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+    }
+    if (on) {
+        float *o = ev.row(c, ag);
+        o[sa] = ang;
+        o[sd] = d;
+    }
+}
+
+// template / obstacle item k2 (< NREST) of finished env c
+template <int A, int O, class Envs>
+__device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, const float *form, int c,
+                                                 int k2)
+{
+    const int64_t e = ev.env(c);
+    if (k2 < 5 * A) {
+        float *d = ev.state(c) + k2;
+        *d = blend_in(*d, form[k2]);
+    } else if (k2 < 5 * A + 2) {
+        const int j = k2 - 5 * A;
+        float *d = ev.targ(c) + j;
+        const float v = blend_in(*d, form[k2]);
+        *d = v;
+        out_el(kl->a.b.target, 2 * e + j, v);
+    } else {
+        const int jb = k2 - (5 * A + 2);
+        uint32_t cc[4];
+        philox_obst_block(cc, jb, (uint64_t)(kl->a.env_offset + e), kl->a.step_idx, kl->p.seed);
+        const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
+        const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
+        float *gob = kl->a.b.obstacles;
+        const int j = 2 * jb;
+        float *o = ev.obst(c) + 2 * j;
+        const int64_t g = e * O * 2 + 2 * j;
+        o[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+        o[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
+        out_el(gob, g, o[0]);
+        out_el(gob, g + 1, o[1]);
+        if (j + 1 < O) {
+            o[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
+            o[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
+            out_el(gob, g + 2, o[2]);
+            out_el(gob, g + 3, o[3]);
+        }
+    }
+}
+
 template <int A, int O, class Envs, class List>
 __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, const float *form,
                                                     const List &list, int nfin, float cap, int tid,
                                                     int nt)
 {
-    constexpr int NP = 1 + O + (A - 1), NB = (O + 1) / 2;
-    constexpr int NPAIR = A * NP, NI = NPAIR + 5 * A + 2 + NB;
-    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
-    const int64_t eoff = kl->a.env_offset;
-    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
-    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
-    float *gob = kl->a.b.obstacles;
-    float *gtg = kl->a.b.target;
+    using IT = NativeItems<A, O>;
+    constexpr int NI = IT::NPAIR + IT::NREST;
+    const int lane = tid & 63, wv = tid >> 6, nwv = nt >> 6;
+    if (nwv >= 2) {
+        const int pw = nwv >> 1;  // waves [0, pw): pair items; [pw, nwv): the rest
+        if (wv < pw) {
+            const int n = nfin * IT::NPAIR;
+            for (int base = 64 * wv; base < n; base += 64 * pw) {
+                const int i = base + lane;
+                const bool on = i < n;
+                const int ic = on ? i : 0;
+                const int fe = ic / IT::NPAIR;
+                native_pair_item<A, O>(kl, ev, form, list[fe], ic - fe * IT::NPAIR, on, cap);
+            }
+        } else {
+            const int n = nfin * IT::NREST;
+            for (int base = 64 * (wv - pw); base < n; base += 64 * (nwv - pw)) {
+                const int i = base + lane;
+                if (i < n) {
+                    const int fe = i / IT::NREST;
+                    native_rest_item<A, O>(kl, ev, form, list[fe], i - fe * IT::NREST);
+                }
+            }
+        }
+        return;
+    }
     const int n = nfin * NI;
-    for (int base = 0; base < n; base += nt) {
-        const int i = base + tid;
+    for (int base = 64 * wv; base < n; base += nt) {
+        const int i = base + lane;
         const bool on = i < n;
         const int ic = on ? i : 0;
         const int fe = ic / NI, kk = ic - fe * NI;
         const int c = list[fe];
-        const int64_t e = ev.env(c);
-        const uint64_t gid = (uint64_t)(eoff + e);
-        const bool pair = kk < NPAIR;
-        // Philox block: obstacle pair items (the block of their obstacle) and
-        // obstacle store items
-        int jb = -1;
-        int ag = 0, p = 0;
-        if (pair) {
-            ag = kk / NP;
-            p = kk - ag * NP;
-            if (p >= 1 && p <= O) jb = (p - 1) >> 1;
-        } else if (kk >= NPAIR + 5 * A + 2) {
-            jb = kk - (NPAIR + 5 * A + 2);
-        }
-        uint32_t cc[4] = {0u, 0u, 0u, 0u};
-        if (jb >= 0) {
-            cc[0] = (uint32_t)jb;
-            cc[1] = (uint32_t)sidx;
-            cc[2] = (uint32_t)gid;
-            cc[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
-            philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
-        }
-        if (pair) {
-            // inputs: the blend of the env's current value (LDS; other items
-            // may be blending it in place meanwhile - blend_in is idempotent)
-            // with its fresh value (template or Philox draw)
-            const float *s = form + 5 * ag;
-            const float *so = ev.state(c) + 5 * ag;
-            const float ox = blend_in(so[0], s[0]), oy = blend_in(so[1], s[1]);
-            const float dx = blend_in(so[2], s[2]), dy = blend_in(so[3], s[3]);
-            float px, py;
-            int sa, sd;
-            if (p == 0) {            // target
-                px = blend_in(ev.targ(c)[0], form[5 * A]);
-                py = blend_in(ev.targ(c)[1], form[5 * A + 1]);
-                sa = 0;
-                sd = 1;
-            } else if (p <= O) {     // obstacle p - 1: components of its Philox block
-                const bool hi = ((p - 1) & 1) != 0;
-                const uint32_t ux = hi ? cc[2] : cc[0], uy = hi ? cc[3] : cc[1];
-                const float *oo = ev.obst(c) + 2 * (p - 1);
-                px = blend_in(oo[0], rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx);
-                py = blend_in(oo[1], ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my);
-                sa = 1 + p;
-                sd = 1 + O + p;
-            } else {                 // other agent kx, skipping self
-                const int kx = p - O - 1;
-                const int m = kx + (kx >= ag ? 1 : 0);
-                const float *q = form + 5 * m;
-                const float *qo = ev.state(c) + 5 * m;
-                px = blend_in(qo[0], q[0]);
-                py = blend_in(qo[1], q[1]);
-                sa = 2 + 2 * O + kx;
-                sd = 2 + 2 * O + (A - 1) + kx;
-            }
-            const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
-            bool unused = true;
-            float d, ang;
-            if (__ballot(on && !cok) == 0ull) {
-                d = pair_dist<true>(ox, oy, px, py, unused);
-                ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
-            } else {
-                d = pair_dist<false>(ox, oy, px, py, unused);
-                ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
-            }
-            if (on) {
-                float *o = ev.row(c, ag);
-                o[sa] = ang;
-                o[sd] = d;
-            }
-        } else if (on) {
-            const int k2 = kk - NPAIR;
-            if (k2 < 5 * A) {
-                float *d = ev.state(c) + k2;
-                *d = blend_in(*d, form[k2]);
-            } else if (k2 < 5 * A + 2) {
-                const int j = k2 - 5 * A;
-                float *d = ev.targ(c) + j;
-                const float v = blend_in(*d, form[k2]);
-                *d = v;
-                out_el(gtg, 2 * e + j, v);
-            } else {
-                const int j = 2 * jb;
-                float *o = ev.obst(c) + 2 * j;
-                const int64_t g = e * O * 2 + 2 * j;
-                o[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
-                o[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
-                out_el(gob, g, o[0]);
-                out_el(gob, g + 1, o[1]);
-                if (j + 1 < O) {
-                    o[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
-                    o[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
-                    out_el(gob, g + 2, o[2]);
-                    out_el(gob, g + 3, o[3]);
-                }
-            }
-        }
+        if (kk < IT::NPAIR)
+            native_pair_item<A, O>(kl, ev, form, c, kk, on, cap);
+        else if (on)
+            native_rest_item<A, O>(kl, ev, form, c, kk - IT::NPAIR);
     }
 }

@@ -880,10 +880,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     STAMP(7);
     if (lane == 0) {
-        g_stamps[(size_t)gw * 24 + 16] = t_entry;
-        g_stamps[(size_t)gw * 24 + 17] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-        g_stamps[(size_t)gw * 24 + 18] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
-        g_stamps[(size_t)gw * 24 + 19] = (unsigned)stamp_nfin;
+        *STAMP_PTR((size_t)gw * 24 + 16) = t_entry;
+        *STAMP_PTR((size_t)gw * 24 + 17) = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        *STAMP_PTR((size_t)gw * 24 + 18) = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+        *STAMP_PTR((size_t)gw * 24 + 19) = (unsigned)stamp_nfin;
     }
 #endif
 }

@@ -11,10 +11,14 @@
 #endif
 #if MARLNAV_STAMPS
 __device__ unsigned long long *g_stamps;
+// global (not flat) stores: a flat store also counts in lgkmcnt, so the next
+// LDS wait would wait for the stamp's write to reach memory
+typedef __attribute__((address_space(1))) unsigned long long stamp_t;
+#define STAMP_PTR(off) ((stamp_t *)(g_stamps) + (off))
 #define STAMP(k)                                                                   \
     do {                                                                           \
         if (lane == 0) {                                                           \
-            unsigned long long *sp_ = g_stamps + (size_t)gw * 24;                  \
+            stamp_t *sp_ = STAMP_PTR((size_t)gw * 24);                             \
             sp_[2 * (k)] = wall_clock64();                                         \
             sp_[2 * (k) + 1] = clock64();                                          \
         }                                                                          \
@@ -22,7 +26,7 @@ __device__ unsigned long long *g_stamps;
 // extra realtime-only stamps at slots 20..23 (diagnostic sub-phases)
 #define STAMPX(k)                                                                  \
     do {                                                                           \
-        if (lane == 0) g_stamps[(size_t)gw * 24 + 20 + (k)] = wall_clock64();      \
+        if (lane == 0) *STAMP_PTR((size_t)gw * 24 + 20 + (k)) = wall_clock64();    \
     } while (0)
 #else
 #define STAMPX(k) \
