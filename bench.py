@@ -22,18 +22,19 @@ clocks, which at the driver's 20-step setting was the difference between
 barrier + synchronize; K timed steps; synchronize + barrier; the max over
 ranks. value = N*P*K / max time.
 
-roofline (the step kernel): ``kernel_us`` = average duration of one step
-launch, from HIP events on the launch stream around replays of a hipGraph of
-back-to-back Env.step launches (of a second Env of the same shape, so the
-timed env's state and counters are untouched); ``achieved`` = algorithmic
-bytes per launch (read 28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at
-A3/O3) / ``kernel_us``, against the 8 TB/s HBM peak. ``timed_region_us`` =
-HIP events on the launch stream around a second, untimed pass of the same K
-steps, per step (includes any gap the host leaves between launches); the
-timed pass itself carries no events (recording one there adds ~13 us of
-GPU-side marker processing per region, scripts/diag/sync_overhead.py). ``traffic``: HBM bytes per launch
-from the committed rocprofv3 PMC summary for this config (profiles/; not
-measured in this run - the source is named), or null.
+roofline (the step kernel): ``launch_us`` = average duration of one step
+launch over the timed steps - HIP events on the launch stream around a second,
+untimed pass of the same K steps (the timed pass itself carries no events:
+recording one there adds ~13 us of GPU-side marker processing per region,
+scripts/diag/sync_overhead.py), so it includes any gap the host leaves
+between launches; ``achieved`` = algorithmic bytes per launch (read
+28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at A3/O3) / ``launch_us``,
+against the 8 TB/s HBM peak. Cross-check: ``graph_replay_launch_us``, the
+same launches back to back from a hipGraph of a second Env of the same shape
+(the timed env's state and counters untouched), which is what a rocprofv3
+kernel duration of back-to-back launches measures. ``traffic``: HBM bytes per
+launch from the committed rocprofv3 PMC summary for this config (profiles/;
+not measured in this run - the source is named), or null.
 
 cpu_baseline (rank 0, N=1): oracle/torch_ref.py - the reference's step
 restated with its own execution structure in eager PyTorch (pinned bit for
@@ -144,12 +145,34 @@ def make_actions(P, A, device, rank, n=64):
     return out
 
 
-def kernel_time_us(env, actions, n=25, replays=12):
+def kernel_time_us(env, actions, n=25, replays=12, per_event=8):
     """Average step-launch duration: HIP events on the launch stream around
-    replays of a hipGraph holding n back-to-back Env.step launches of ``env``
-    (each interval includes the graph's inter-kernel boundary, as a
-    back-to-back rocprofv3 kernel duration does). Returns (mean, median)."""
+    ``per_event`` back-to-back replays of a hipGraph holding n Env.step
+    launches of ``env`` (each interval includes the graph's inter-kernel
+    boundary, as a back-to-back rocprofv3 kernel duration does; the ~13 us an
+    event pair adds on the GPU is spread over n * per_event launches).
+    ``replays`` such measurements; returns (mean, median) in us per launch."""
     env.allow_graph_capture = True  # replays repeat the captured re-init draws: timing only
+    graph = capture_steps(env, actions, n)
+    graph.replay()
+    torch.cuda.synchronize()
+    per = []
+    for _ in range(replays):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(per_event):
+            graph.replay()
+        e.record()
+        e.synchronize()
+        per.append(s.elapsed_time(e) * 1e3 / (n * per_event))
+    per.sort()
+    return sum(per) / len(per), per[len(per) // 2]
+
+
+def capture_steps(env, actions, n):
+    """A hipGraph of n back-to-back Env.step launches of ``env`` (which must
+    allow graph capture; replays repeat the captured re-init draws)."""
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -161,31 +184,25 @@ def kernel_time_us(env, actions, n=25, replays=12):
     with torch.cuda.graph(graph):
         for i in range(n):
             env.step(actions[i % len(actions)])
-    graph.replay()
-    torch.cuda.synchronize()
-    per = []
-    for _ in range(replays):
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        s.record()
-        graph.replay()
-        e.record()
-        e.synchronize()
-        per.append(s.elapsed_time(e) * 1e3 / n)
-    per.sort()
-    return sum(per) / len(per), per[len(per) // 2]
+    return graph
 
 
 def prewarm(env, actions, seconds):
-    """Back-to-back steps of a scratch Env for ``seconds`` (GPU clock ramp;
-    nothing of the timed Env runs here). Returns the steps taken."""
+    """GPU clock ramp: back-to-back steps of a scratch Env for ``seconds``
+    (nothing of the timed Env runs here), as replays of a hipGraph of 64
+    steps, so the GPU stays busy without host gaps (under rocprofv3, whose
+    per-launch host overhead exceeds a step, host-launched steps would run
+    isolated). Returns the steps taken."""
+    env.allow_graph_capture = True  # scratch Env: the replays' repeated draws are irrelevant
+    graph = capture_steps(env, actions, 64)
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        for _ in range(64):
-            env.step(actions[n % len(actions)])
-            n += 1
+        for _ in range(8):
+            graph.replay()
+            n += 64
         torch.cuda.synchronize()
+    env.allow_graph_capture = False
     return n
 
 
@@ -352,7 +369,9 @@ def main():
     del kenv
     per_env = alg_bytes_per_env(A, O)
     launch_bytes = per_env * P
-    achieved = launch_bytes / (kern_us * 1e-6) / 1e9
+    # the step kernel's average launch duration over the timed steps (HIP
+    # events on the launch stream; includes any inter-launch gap)
+    achieved = launch_bytes / (region_us * 1e-6) / 1e9
     traffic, traffic_src = load_traffic(a.pmc, f"P{P}_A{A}_O{O}")
 
     cpu = None
@@ -383,8 +402,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel_us": kern_us, "kernel_us_median": kern_med,
-                         "timed_region_us": region_us,
+                         "launch_us": region_us,
+                         "graph_replay_launch_us": kern_us,
+                         "graph_replay_launch_us_median": kern_med,
                          "alg_bytes_per_launch": launch_bytes,
                          "alg_bytes_per_env_step": per_env},
             "cpu_baseline": cpu,

@@ -340,9 +340,29 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
 // NaN -> quadrant 0 (NaN propagates); sin(-0) = -0. The identical operation
 // sequence (explicit FMAs, no contraction) is oracle_sincos in
 // oracle/marlnav_oracle.c, so kernel and oracle agree bit for bit.
+// A wave whose angles all lie in |th| < 0.78 (< pi/4: quadrant k = 0 on
+// every lane, the common case) skips the reduction and the quadrant selects:
+// the same operations on r = x, so the same bits.
 __device__ __forceinline__ void sincos_k(float th, float *s_out, float *c_out)
 {
     const double x = (double)th;
+    if (!(MARLNAV_AB & 32) && __ballot(!(fabsf(th) < 0.78f)) == 0ull) {
+        const double z = x * x;
+        double ps = __builtin_fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+        ps = __builtin_fma(z, ps, 2.75573137070700676789e-06);
+        ps = __builtin_fma(z, ps, -1.98412698298579493134e-04);
+        ps = __builtin_fma(z, ps, 8.33333333332248946124e-03);
+        ps = __builtin_fma(z, ps, -1.66666666666666324348e-01);
+        const double sd = x == 0.0 ? x : __builtin_fma(z * x, ps, x);
+        double pc = __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+        pc = __builtin_fma(z, pc, -2.75573143513906633035e-07);
+        pc = __builtin_fma(z, pc, 2.48015872894767294178e-05);
+        pc = __builtin_fma(z, pc, -1.38888888888741095749e-03);
+        pc = __builtin_fma(z, pc, 4.16666666666666019037e-02);
+        *s_out = (float)sd;
+        *c_out = (float)__builtin_fma(z * z, pc, __builtin_fma(-0.5, z, 1.0));
+        return;
+    }
     const double k = __builtin_rint(x * 6.36619772367581382433e-01);
     double r = __builtin_fma(-k, 1.57079632673412561417e+00, x);
     r = __builtin_fma(-k, 6.07710050650619224932e-11, r);

@@ -32,8 +32,8 @@ struct BlockPlan {
     static constexpr int OBS = RED + 4 * R;                // (R, D) packed rows
     static constexpr int LIST = (OBS + R * D + 3) & ~3;    // (E,) finished envs
     static constexpr int FLG = LIST + E;                   // [0] nfin, [1 + w] wave w coords bad
-    static constexpr int LIST2 = (FLG + 1 + A + 3) & ~3;   // (A-1, E) finished envs, waves >= 1
-    static constexpr int FLOATS = (LIST2 + (A - 1) * E + 3) & ~3;
+    static constexpr int FRESH = (FLG + 1 + A + 3) & ~3;   // (2O, E) fresh obstacle draws
+    static constexpr int FLOATS = FRESH + 2 * O * E;
     static_assert(A >= 2 && A <= 16, "one wave per agent");
 };
 
@@ -177,6 +177,36 @@ __global__ void __launch_bounds__(64 * A)
     }
     const MarlnavParams pr = load_params(K);
     const bool wt = (pr.flags & kWriteThroughFlag) != 0;  // written-through outputs
+    // native (non-noisy) re-init: waves 1..A-1 take the finished envs while
+    // wave 0 runs the per-env phase (below)
+    const bool overlap = !OBS_ONLY && !NOISY && !K->a.b.fresh_states;
+    // (one Philox block per thread at most: at A3/O8 the two passes cost the
+    // stage phase more than they save, 131072x3x8 18.4 -> 19.0 us)
+    constexpr bool kPre = E * ((O + 1) / 2) <= NT;
+    if (kPre && overlap) {
+        // the fresh obstacles of every env of the block (its Philox draws
+        // depend only on seed, step and env id), drawn while the staging
+        // loads are in flight: a finished env's re-init then reads them
+        // instead of drawing after the per-env barrier, where the draws sat
+        // on the block's critical path (65536x3x3: 0.25 us of 0.63)
+        KArgsK *kl = kargs_late<kHotKargsOff>();
+        const uint64_t sidx = kl->a.step_idx, g0 = (uint64_t)(kl->a.env_offset + e0);
+        constexpr int NB = (O + 1) / 2;
+        float *pre = lds + BP::FRESH;
+#pragma unroll
+        for (int k2 = 0; k2 * NT < E * NB; ++k2) {
+            const int i = tid + k2 * NT;
+            const int l = i % E, jb = i / E;
+            if (((k2 + 1) * NT <= E * NB || i < E * NB) && l < ne) {
+                float v[4];
+                native_obst_draws(pr.seed, sidx, g0 + l, jb, pr.obs_range_x, pr.obs_mean_x,
+                                  pr.obs_range_y, pr.obs_mean_y, v);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (2 * jb + k / 2 < O) pre[(4 * jb + k) * E + l] = v[k];
+            }
+        }
+    }
     const int l = (int)lane;  // env of this lane within the block
     const int r = l * A + w;  // row of this lane
     const bool row_on = l < ne;
@@ -286,9 +316,6 @@ __global__ void __launch_bounds__(64 * A)
         int *list = reinterpret_cast<int *>(lds + BP::LIST);
         int *flg = reinterpret_cast<int *>(lds + BP::FLG);
         const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
-        // native (non-noisy) re-init: waves 1..A-1 take the finished envs
-        // while wave 0 runs the per-env phase (below)
-        const bool overlap = !NOISY && !kargs_late<kHotKargsOff>()->a.b.fresh_states;
         // ---- per-env reductions, terminal logic (wave 0, one lane per env)
         if (w == 0) {
             const bool env_on = l < ne;
@@ -386,14 +413,11 @@ __global__ void __launch_bounds__(64 * A)
             const uint64_t fm = __ballot(fin);
             STAMPX(0);
             if (fm && !(MARLNAV_AB & 1)) {
-                int *wlist = reinterpret_cast<int *>(lds + BP::LIST2) + E * (w - 1);
-                if (fin)
-                    wlist[__builtin_amdgcn_mbcnt_hi(
-                        (unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] = l;
-                wave_sync();  // every lane of this wave sees its list
                 STAMPX(1);
-                reinit_reobs_native<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, wlist,
-                                          (int)__popcll(fm), pr.cap_distance, tid - 64, NT - 64);
+                reinit_reobs_native<A, O, kPre ? E : 0>(kargs_late<kHotKargsOff>(), ev,
+                                                        lds + BP::FORM, MaskList{fm},
+                                                        (int)__popcll(fm), pr.cap_distance,
+                                                        tid - 64, NT - 64, lds + BP::FRESH);
                 STAMPX(2);
             }
         }

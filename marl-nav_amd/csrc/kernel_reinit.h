@@ -152,6 +152,32 @@ __device__ __forceinline__ void lds_row_write(float *dst, const float *row)
     }
 }
 
+__device__ __forceinline__ void philox_obst_block(uint32_t cc[4], int jb, uint64_t gid, uint64_t sidx,
+                                                  uint64_t seed)
+{
+    cc[0] = (uint32_t)jb;
+    cc[1] = (uint32_t)sidx;
+    cc[2] = (uint32_t)gid;
+    cc[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
+    if (!(MARLNAV_AB & 4)) philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// The block's fresh obstacle draws precomputed while its staging loads are in
+// flight (env-block kernel; the split kernel draws in the items): `pre` holds
+// component k (0 x, 1 y) of obstacle j of env code c at pre[(2j + k) * E + c].
+// The Philox block jb of env gid, as native_fresh_env draws it, scaled into
+// obstacle coordinates.
+__device__ __forceinline__ void native_obst_draws(uint64_t seed, uint64_t sidx, uint64_t gid, int jb,
+                                                  float rx, float mx, float ry, float my, float v[4])
+{
+    uint32_t cc[4];
+    philox_obst_block(cc, jb, gid, sidx, seed);
+    v[0] = rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+    v[1] = ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
+    v[2] = rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
+    v[3] = ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
+}
+
 // Re-initialisation of the finished envs (environment.py:76-90, the sampler
 // call at :78) spread over the workgroup: one item per thread per pass - one
 // float of a fresh candidate (reference RNG) or of the formation template,
@@ -162,10 +188,12 @@ __device__ __forceinline__ void lds_row_write(float *dst, const float *row)
 // blended agent coordinates or target differ from the formation's bits (a
 // non-finite old value blends to NaN), i.e. when the formation template
 // (reobs_block_tpl) does not describe the re-initialised env.
-template <int A, int O, class Envs, class List>
+// E > 0 (native re-init): the fresh obstacles come from `pre` (E envs,
+// native_obst_draws at stage time) instead of being drawn here.
+template <int A, int O, int E = 0, class Envs, class List>
 __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const float *form,
                                              const List &list, int nfin, int tid, int nt,
-                                             int *unclean = nullptr)
+                                             int *unclean = nullptr, const float *pre = nullptr)
 {
     float *gob = kl->a.b.obstacles;
     float *gtg = kl->a.b.target;
@@ -221,20 +249,23 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
             if (unclean && __float_as_uint(v) != __float_as_uint(form[kk])) *unclean = 1;
         } else {
             const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
-            const uint64_t gid = (uint64_t)(eoff + e);
-            uint32_t cc[4] = {(uint32_t)jb, (uint32_t)sidx, (uint32_t)gid,
-                              (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
-            philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
             const int j = 2 * jb;
+            float v[4];
+            if constexpr (E > 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = (j + k / 2 < O) ? pre[(2 * j + k) * E + c] : 0.0f;
+            } else {
+                native_obst_draws(seed, sidx, (uint64_t)(eoff + e), jb, rx, mx, ry, my, v);
+            }
             float *o = ev.obst(c) + 2 * j;
             const int64_t g = e * O * 2 + 2 * j;
-            o[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
-            o[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
+            o[0] = blend_in(o[0], v[0]);
+            o[1] = blend_in(o[1], v[1]);
             out_el(gob, g, o[0]);
             out_el(gob, g + 1, o[1]);
             if (j + 1 < O) {
-                o[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
-                o[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
+                o[2] = blend_in(o[2], v[2]);
+                o[3] = blend_in(o[3], v[3]);
                 out_el(gob, g + 2, o[2]);
                 out_el(gob, g + 3, o[3]);
             }
@@ -262,27 +293,20 @@ struct NativeItems {
     static constexpr int NPAIR = A * NP, NREST = 5 * A + 2 + NB;
 };
 
-__device__ __forceinline__ void philox_obst_block(uint32_t cc[4], int jb, uint64_t gid, uint64_t sidx,
-                                                  uint64_t seed)
-{
-    cc[0] = (uint32_t)jb;
-    cc[1] = (uint32_t)sidx;
-    cc[2] = (uint32_t)gid;
-    cc[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
-    philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
-}
 
-// pair item kk (< NPAIR) of finished env c; `on` false: computes, stores nothing
-template <int A, int O, class Envs>
-__device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, const float *form, int c,
-                                                 int kk, bool on, float cap)
+// pair item kk (< NPAIR) of finished env c; `on` false: computes, stores nothing.
+// PRE: fresh obstacles from `pre` (E envs per block), else drawn here.
+template <int A, int O, int E, class Envs>
+__device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, const float *form,
+                                                 const float *pre, int c, int kk, bool on, float cap)
 {
     using IT = NativeItems<A, O>;
     const int ag = kk / IT::NP, p = kk - ag * IT::NP;
     uint32_t cc[4] = {0u, 0u, 0u, 0u};
-    if (p >= 1 && p <= O)  // obstacle p - 1: its Philox block
-        philox_obst_block(cc, (p - 1) >> 1, (uint64_t)(kl->a.env_offset + ev.env(c)), kl->a.step_idx,
-                          kl->p.seed);
+    const bool cargs = (MARLNAV_AB & 8) != 0;  // timing only: no kernel-argument loads
+    if (!E && p >= 1 && p <= O)  // obstacle p - 1: its Philox block
+        philox_obst_block(cc, (p - 1) >> 1, (uint64_t)((cargs ? 0 : kl->a.env_offset) + ev.env(c)),
+                          cargs ? 7u : kl->a.step_idx, cargs ? 5u : kl->p.seed);
     // inputs: the blend of the env's current value (LDS; other items may be
     // blending it in place meanwhile - blend_in is idempotent) with its fresh
     // value (template or Philox draw)
@@ -298,11 +322,18 @@ __device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, con
         sa = 0;
         sd = 1;
     } else if (p <= O) {     // obstacle p - 1: components of its Philox block
-        const bool hi = ((p - 1) & 1) != 0;
-        const uint32_t ux = hi ? cc[2] : cc[0], uy = hi ? cc[3] : cc[1];
         const float *oo = ev.obst(c) + 2 * (p - 1);
-        px = blend_in(oo[0], kl->p.obs_range_x * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + kl->p.obs_mean_x);
-        py = blend_in(oo[1], kl->p.obs_range_y * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + kl->p.obs_mean_y);
+        if constexpr (E > 0) {
+            px = blend_in(oo[0], pre[(2 * (p - 1)) * E + c]);
+            py = blend_in(oo[1], pre[(2 * (p - 1) + 1) * E + c]);
+        } else {
+            const bool hi = ((p - 1) & 1) != 0;
+            const uint32_t ux = hi ? cc[2] : cc[0], uy = hi ? cc[3] : cc[1];
+            const float rx = cargs ? 1000.f : kl->p.obs_range_x, mx = cargs ? 0.f : kl->p.obs_mean_x;
+            const float ry = cargs ? 1000.f : kl->p.obs_range_y, my = cargs ? 0.f : kl->p.obs_mean_y;
+            px = blend_in(oo[0], rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx);
+            py = blend_in(oo[1], ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my);
+        }
         sa = 1 + p;
         sd = 1 + O + p;
     } else {                 // other agent kx, skipping self
@@ -318,7 +349,10 @@ __device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, con
     const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
     bool unused = true;
     float d, ang;
-    if (__ballot(on && !cok) == 0ull) {
+    if (MARLNAV_AB & 16) {  // timing only: no pair math
+        d = px + ox + dx;
+        ang = py + oy + dy;
+    } else if (__ballot(on && !cok) == 0ull) {
         d = pair_dist<true>(ox, oy, px, py, unused);
         ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
     } else {
@@ -332,10 +366,10 @@ __device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, con
     }
 }
 
-// template / obstacle item k2 (< NREST) of finished env c
-template <int A, int O, class Envs>
-__device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, const float *form, int c,
-                                                 int k2)
+// template / obstacle item k2 (< NREST) of finished env c (PRE as above)
+template <int A, int O, int E, class Envs>
+__device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, const float *form,
+                                                 const float *pre, int c, int k2)
 {
     const int64_t e = ev.env(c);
     if (k2 < 5 * A) {
@@ -349,35 +383,70 @@ __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, con
         out_el(kl->a.b.target, 2 * e + j, v);
     } else {
         const int jb = k2 - (5 * A + 2);
-        uint32_t cc[4];
-        philox_obst_block(cc, jb, (uint64_t)(kl->a.env_offset + e), kl->a.step_idx, kl->p.seed);
-        const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
-        const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
-        float *gob = kl->a.b.obstacles;
         const int j = 2 * jb;
+        float v[4];
+        if constexpr (E > 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = (j + k / 2 < O) ? pre[(2 * j + k) * E + c] : 0.0f;
+        } else {
+            native_obst_draws(kl->p.seed, kl->a.step_idx, (uint64_t)(kl->a.env_offset + e), jb,
+                              kl->p.obs_range_x, kl->p.obs_mean_x, kl->p.obs_range_y,
+                              kl->p.obs_mean_y, v);
+        }
+        float *gob = kl->a.b.obstacles;
         float *o = ev.obst(c) + 2 * j;
         const int64_t g = e * O * 2 + 2 * j;
-        o[0] = blend_in(o[0], rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx);
-        o[1] = blend_in(o[1], ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my);
+        o[0] = blend_in(o[0], v[0]);
+        o[1] = blend_in(o[1], v[1]);
         out_el(gob, g, o[0]);
         out_el(gob, g + 1, o[1]);
         if (j + 1 < O) {
-            o[2] = blend_in(o[2], rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx);
-            o[3] = blend_in(o[3], ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my);
+            o[2] = blend_in(o[2], v[2]);
+            o[3] = blend_in(o[3], v[3]);
             out_el(gob, g + 2, o[2]);
             out_el(gob, g + 3, o[3]);
         }
     }
 }
 
-template <int A, int O, class Envs, class List>
+// The finished envs of a block as a wave-uniform ballot mask (env code = bit
+// position; the env-block kernel): entry fe is the fe-th set bit, found by
+// scalar bit scans over the few entries one pass of items touches - no LDS
+// list to write, wait for and read back.
+struct MaskList {
+    uint64_t fm;
+};
+
+// env code of entry fe, for the entries [lo, hi] of one pass (wave-uniform)
+template <class List>
+__device__ __forceinline__ int list_code(const List &l, int fe, int, int)
+{
+    return l[fe];
+}
+
+__device__ __forceinline__ int list_code(const MaskList &l, int fe, int lo, int hi)
+{
+    uint64_t m = l.fm;
+    for (int f = 0; f < lo; ++f) m &= m - 1;
+    int c = 0;
+    for (int f = lo; f <= hi; ++f) {
+        const int pos = (int)__builtin_ctzll(m);
+        c = fe == f ? pos : c;
+        m &= m - 1;
+    }
+    return c;
+}
+
+// E > 0: fresh obstacles precomputed in `pre` (E envs, native_obst_draws)
+template <int A, int O, int E = 0, class Envs, class List>
 __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, const float *form,
                                                     const List &list, int nfin, float cap, int tid,
-                                                    int nt)
+                                                    int nt, const float *pre = nullptr)
 {
     using IT = NativeItems<A, O>;
     constexpr int NI = IT::NPAIR + IT::NREST;
-    const int lane = tid & 63, wv = tid >> 6, nwv = nt >> 6;
+    // (tid and nt are wave-aligned: the wave index is uniform)
+    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), nwv = nt >> 6;
     if (nwv >= 2) {
         const int pw = nwv >> 1;  // waves [0, pw): pair items; [pw, nwv): the rest
         if (wv < pw) {
@@ -387,16 +456,18 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
                 const bool on = i < n;
                 const int ic = on ? i : 0;
                 const int fe = ic / IT::NPAIR;
-                native_pair_item<A, O>(kl, ev, form, list[fe], ic - fe * IT::NPAIR, on, cap);
+                const int lo = base / IT::NPAIR, hi = min((base + 63) / IT::NPAIR, nfin - 1);
+                native_pair_item<A, O, E>(kl, ev, form, pre, list_code(list, fe, lo, hi),
+                                          ic - fe * IT::NPAIR, on, cap);
             }
         } else {
             const int n = nfin * IT::NREST;
             for (int base = 64 * (wv - pw); base < n; base += 64 * (nwv - pw)) {
                 const int i = base + lane;
-                if (i < n) {
-                    const int fe = i / IT::NREST;
-                    native_rest_item<A, O>(kl, ev, form, list[fe], i - fe * IT::NREST);
-                }
+                const int lo = base / IT::NREST, hi = min((base + 63) / IT::NREST, nfin - 1);
+                const int fe = (i < n ? i : 0) / IT::NREST;
+                const int c = list_code(list, fe, lo, hi);
+                if (i < n) native_rest_item<A, O, E>(kl, ev, form, pre, c, i - fe * IT::NREST);
             }
         }
         return;
@@ -407,10 +478,10 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
         const bool on = i < n;
         const int ic = on ? i : 0;
         const int fe = ic / NI, kk = ic - fe * NI;
-        const int c = list[fe];
+        const int c = list_code(list, fe, base / NI, min((base + 63) / NI, nfin - 1));
         if (kk < IT::NPAIR)
-            native_pair_item<A, O>(kl, ev, form, c, kk, on, cap);
+            native_pair_item<A, O, E>(kl, ev, form, pre, c, kk, on, cap);
         else if (on)
-            native_rest_item<A, O>(kl, ev, form, c, kk - IT::NPAIR);
+            native_rest_item<A, O, E>(kl, ev, form, pre, c, kk - IT::NPAIR);
     }
 }

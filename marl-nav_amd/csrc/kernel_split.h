@@ -167,7 +167,12 @@ struct SplitPlan {
     // the workgroup's per-env inputs, parked for wave 0's per-env phase)
     static constexpr int ENVIN = (kWavesPerBlock * (1 + EPW) + 1 + 3) & ~3;
     static constexpr int FTP = (ENVIN + 2 * kWavesPerBlock * EPW + 3) & ~3;
-    static constexpr int BLK = FTP + (kSplitTpl<A, O> ? NCP : 0);
+    // then (kSplitSpread shapes, native re-init) the fresh obstacle draws of
+    // the workgroup's EW envs, component k of obstacle j of env code c at
+    // PRE + (2j + k) * EW + c (kernel_reinit.h native_obst_draws)
+    static constexpr int EW = kWavesPerBlock * EPW;
+    static constexpr int PRE = (FTP + (kSplitTpl<A, O> ? NCP : 0) + 3) & ~3;
+    static constexpr int BLK = PRE + (kSplitSpread<A, O> && O <= 8 ? 2 * O * EW : 0);
     static_assert(EPW >= 1, "an env's rows must fit one wave");
 };
 
@@ -402,6 +407,34 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     }
     const MarlnavParams pr = load_params(K);
     const bool wt = (pr.flags & kWriteThroughFlag) != 0;  // written-through outputs
+    float *const pre = lds + kWavesPerBlock * SP::FLOATS + SP::PRE;
+    // (the fused native re-init of few-obstacle shapes only: at A16/O32 the
+    // draws cost the stage more than they save, 4096x16x32 12.62 -> 12.76 us)
+    constexpr bool kPre = kSplitSpread<A, O> && O <= 8;
+    if constexpr (kPre && !NOISY && !OBS_ONLY) {
+        // native re-init: this wave's envs' fresh obstacles (Philox draws of
+        // seed, step and env id), drawn while the staging loads are in
+        // flight, so a finished env's workgroup-spread re-init reads them
+        // instead of drawing after the per-env barrier
+        KArgsK *kl = kargs_late<kHotKargsOff>();
+        if (!kl->a.b.fresh_states) {
+            const uint64_t sidx = kl->a.step_idx, g0 = (uint64_t)(kl->a.env_offset + e0);
+            constexpr int NB = (O + 1) / 2;
+#pragma unroll
+            for (int k2 = 0; k2 * 64 < EPW * NB; ++k2) {
+                const int i = (int)lane + 64 * k2;
+                const int cl = i % EPW, jb = i / EPW;
+                if (((k2 + 1) * 64 <= EPW * NB || i < EPW * NB) && cl < ne) {
+                    float v[4];
+                    native_obst_draws(pr.seed, sidx, g0 + cl, jb, pr.obs_range_x, pr.obs_mean_x,
+                                      pr.obs_range_y, pr.obs_mean_y, v);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (2 * jb + k / 2 < O) pre[(4 * jb + k) * SP::EW + wib * EPW + cl] = v[k];
+                }
+            }
+        }
+    }
     const int row = (int)lane / LPR, q = (int)lane - row * LPR;
     const int rowc = row < R ? row : 0;  // idle lanes shadow row 0 (results unused)
     const int el = rowc / A, a = rowc - el * A;
@@ -687,7 +720,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 #if MARLNAV_STAMPS
             stamp_nfin = list.total();
 #endif
-            if (const int nfin = list.total()) {
+            if (const int nfin = (MARLNAV_AB & 1) ? 0 : list.total()) {  // (AB 1: timing only)
                 KArgsK *kl = kargs_late<kHotKargsOff>();
                 const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
                     lds, blk0 * EPW};
@@ -696,8 +729,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 // fused native re-init + re-observation recomputes a Philox
                 // block per obstacle pair: only for few obstacles
                 if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
-                    reinit_reobs_native<A, O>(kl, ev, kl->a.b.formation, list, nfin,
-                                              pr.cap_distance, tid, nt);
+                    reinit_reobs_native<A, O, SP::EW>(kl, ev, kl->a.b.formation, list, nfin,
+                                                      pr.cap_distance, tid, nt, pre);
                 } else if (kSplitTpl<A, O> && tpl_on) {
                     // formation + template to LDS (from the registers when all
                     // the block's waves are live, else straight from global)
@@ -725,7 +758,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                         reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
                 } else {
                     if (!NOISY) {
-                        reinit_block<A, O>(kl, ev, kl->a.b.formation, list, nfin, tid, nt);
+                        reinit_block<A, O, kPre ? SP::EW : 0>(kl, ev, kl->a.b.formation, list, nfin,
+                                                              tid, nt, nullptr, pre);
                         __syncthreads();
                     }
                     reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);

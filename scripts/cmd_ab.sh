@@ -1,7 +1,14 @@
-# parity suite, then graph-replay A/B of libmarlnav.so against other builds
-# (scripts/build_variant.sh makes them; LIBS lists them, CFGS the configs)
-export TMPDIR=/tmp
+#!/bin/bash
+# GPU tests (optional), then a same-box A/B (graph replay, steady mix of
+# finished envs) of the product build against $LIBS at $CFGS.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+if [ "${TESTS:-1}" = 1 ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${K:+-k "$K"} > gpurun_out/pytest_gpu.txt 2>&1
+  rc=$?; tail -n 8 gpurun_out/pytest_gpu.txt | cut -c1-400; [ $rc = 0 ] || exit $rc
+fi
 L=marl-nav_amd/lib
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pt.log
-case $rc in 0) ;; *) exit $rc;; esac
-timeout -k 10 300 python scripts/graph_time.py ${CFGS:-4096x16x32,512x16x32,1024x3x8,65536x3x3} $L/libmarlnav.so ${LIBS:-$L/ref.so} > gpurun_out/ab.log 2>&1
+args=""; for x in ${LIBS:-}; do args="$args $L/$x"; done
+timeout -k 10 500 python scripts/ab_steady.py "${CFGS:-65536x3x3}" $L/libmarlnav.so $args > gpurun_out/ab.txt 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/ab.txt; exit $rc

@@ -112,6 +112,22 @@ def main():
                                   "end_max_us": round(float(fin_t[m].max()), 2),
                                   "phase_median_us": {n: round(float(np.median(ph[m, i])), 2)
                                                       for i, n in enumerate(names)}})
+        # sub-phase stamps (STAMPX slots 20..23, realtime only) of waves in
+        # tiles with finished envs: medians of consecutive differences, from
+        # the phase-3 stamp (observed) through the X slots to the phase-5 stamp
+        if reo.any():
+            x = raw[reo][:, 20:24] * 10.0 / 1e3
+            t3 = rt[reo][:, 3]
+            t5 = rt[reo][:, 5]
+            seq = [("observed", t3)] + [(f"x{k}", x[:, k]) for k in range(4)] + [("reobs_end", t5)]
+            out = {}
+            prev_name, prev = seq[0]
+            for name, t in seq[1:]:
+                m = (t > 0) & (prev > 0)
+                if m.any():
+                    out[f"{prev_name}->{name}"] = round(float(np.median(t[m] - prev[m])), 3)
+                    prev_name, prev = name, t
+            print(cfg, "with_reobs sub-phases (median us):", out)
         del env
 
 
