@@ -200,23 +200,22 @@ __device__ __forceinline__ bool tile_coords_ok(const float *ob, const float *tg,
     return ok;
 }
 
-// Correctly rounded sqrt for x in [2^-96, 2^96] or x == 0: hipcc's own
-// IEEE sequence (v_sqrt_f32, then the neighbour whose residual straddles x)
-// without its input scaling and special-value class fix-up, which only act
-// outside that range; `ok` is cleared outside it (the caller redoes the row
-// with the full sequence).
+// Correctly rounded sqrt for x in [2^-96, 2^96] or x == 0, in six VALU: the
+// reciprocal square root estimate y, s = x*y, one Newton correction
+// s + (x - s*s) * y/2 (the residual exact by FMA), then max(., 0), which maps
+// x == 0 (0 * inf = NaN) to +0 and is one v_max on an FMA result. Equal to
+// the IEEE sqrtf (hipcc's v_sqrt + two-neighbour residual fix-up, nine VALU)
+// on every float of the range and zero: checked exhaustively on the GPU
+// (scripts/probes/sqrt_rsq_probe.hip, profiles/r03_sqrt_rsq_probe.txt).
+// `ok` is cleared outside the range (the caller redoes the row with IEEE
+// sqrt).
 __device__ __forceinline__ float sqrt_fast(float x, bool &ok)
 {
     ok &= (x >= 0x1p-96f && x <= 0x1p96f) || x == 0.0f;
-    float s = __builtin_amdgcn_sqrtf(x);
-    const float s_dn = __int_as_float(__float_as_int(s) - 1);
-    const float s_up = __int_as_float(__float_as_int(s) + 1);
-    // x - s_dn*s with the sign on the float operand (a free source modifier;
-    // negating the integer-built neighbour costs a v_xor per pair)
-    const float r_dn = __builtin_fmaf(s_dn, -s, x);
-    const float r_up = __builtin_fmaf(s_up, -s, x);
-    s = r_dn <= 0.0f ? s_dn : s;
-    return r_up > 0.0f ? s_up : s;
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s = x * y, h = 0.5f * y;
+    const float e = __builtin_fmaf(-s, s, x);
+    return __builtin_fmaxf(__builtin_fmaf(e, h, s), 0.0f);
 }
 
 // torch.cdist direct path (environment.py:271-274)
@@ -224,6 +223,7 @@ template <bool FAST = false>
 __device__ __forceinline__ float pair_dist(float ox, float oy, float px, float py, bool &ok)
 {
     const float dx = px - ox, dy = py - oy;
+    if (FAST && (MARLNAV_AB & 64)) return dx + dy;  // timing only: trivial pair math
     if constexpr (FAST)
         return sqrt_fast(__builtin_fmaf(dy, dy, dx * dx), ok);
     else
@@ -305,6 +305,7 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
                                             bool &ok)
 {
     const float dx = px - ox, dy = py - oy;
+    if (FAST && (MARLNAV_AB & 64)) return dx * dirx + dist;  // timing only: trivial pair math
     // F.normalize's clamp_min(1e-12). FAST (finite, non-negative dist): one
     // v_med3 instead of a canonicalize + v_max
     const float den = FAST ? __builtin_amdgcn_fmed3f(dist, 1e-12f, __builtin_inff())
@@ -346,6 +347,11 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
 __device__ __forceinline__ void sincos_k(float th, float *s_out, float *c_out)
 {
     const double x = (double)th;
+    if (MARLNAV_AB & 128) {  // timing only: no sin/cos
+        *s_out = th;
+        *c_out = 1.0f - th;
+        return;
+    }
     if (!(MARLNAV_AB & 32) && __ballot(!(fabsf(th) < 0.78f)) == 0ull) {
         const double z = x * x;
         double ps = __builtin_fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);

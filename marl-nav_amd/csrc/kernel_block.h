@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(64 * A)
     // (one Philox block per thread at most: at A3/O8 the two passes cost the
     // stage phase more than they save, 131072x3x8 18.4 -> 19.0 us)
     constexpr bool kPre = E * ((O + 1) / 2) <= NT;
-    if (kPre && overlap) {
+    if (kPre && overlap && !(MARLNAV_AB & 256)) {  // (AB 256: timing only, no draws)
         // the fresh obstacles of every env of the block (its Philox draws
         // depend only on seed, step and env id), drawn while the staging
         // loads are in flight: a finished env's re-init then reads them

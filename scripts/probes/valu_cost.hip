@@ -15,6 +15,8 @@ __global__ void __launch_bounds__(256) run(int iters, float *out, float seed, ui
 {
     typedef float v2 __attribute__((ext_vector_type(2)));
     float a[8], b = seed * 0.5f + 1.0f;
+    double d[8], db = (double)seed * 0.25 + 1.0;
+    for (int i = 0; i < 8; ++i) d[i] = (double)seed + (double)(threadIdx.x + i);
     v2 pa[8], pb = v2{b, b};
     for (int i = 0; i < 8; ++i) pa[i] = v2{seed + (float)i, seed - (float)threadIdx.x};
     for (int i = 0; i < 8; ++i) a[i] = seed + (float)(threadIdx.x + i);
@@ -42,12 +44,20 @@ __global__ void __launch_bounds__(256) run(int iters, float *out, float seed, ui
     if constexpr (M == 14) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "s"(bs), "v"(b)); \
     if constexpr (M == 15) asm volatile("v_cmp_gt_f32_e64 vcc, %0, %1" ::"v"(a[i]), "v"(b) : "vcc"); \
     if constexpr (M == 16) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(pa[i]) : "v"(pb)); \
-    if constexpr (M == 17) asm volatile("v_mov_b32_e32 %0, %1" : "=v"(a[i]) : "v"(a[(i + 1) & 7]));
+    if constexpr (M == 17) asm volatile("v_mov_b32_e32 %0, %1" : "=v"(a[i]) : "v"(a[(i + 1) & 7]));  \
+    if constexpr (M == 18) asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(d[i]) : "v"(a[i]), "v"(b) : "s0", "s1"); \
+    if constexpr (M == 19) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(d[i]) : "v"(db));        \
+    if constexpr (M == 20) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b));           \
+    if constexpr (M == 21) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b));           \
+    if constexpr (M == 22) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b));      \
+    if constexpr (M == 23) asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(b));          \
+    if constexpr (M == 24) asm volatile("v_alignbit_b32 %0, %0, %0, 13" : "+v"(a[i]));              \
+    if constexpr (M == 25) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(d[i]) : "v"(db));
         REP8(OP)
 #undef OP
     }
     float s = 0.0f;
-    for (int i = 0; i < 8; ++i) s += a[i] + pa[i].x + pa[i].y;
+    for (int i = 0; i < 8; ++i) s += a[i] + pa[i].x + pa[i].y + (float)d[i];
     if (s == 12345.678f) out[threadIdx.x] = s;
 }
 
@@ -56,7 +66,9 @@ static const char *kNames[] = {"v_fma_f32 vvv", "v_fmaak_f32 (literal)", "v_mul_
                                "v_cndmask_e32 vcc", "v_cmp_gt_e64 ->sgpr", "v_cmp_gt_e32 ->vcc",
                                "v_sqrt_f32", "v_rcp_f32", "v_fma_f32 |x| consts",
                                "v_sub_f32", "v_fma_f32 sgpr operand", "v_cmp_gt_e64 ->vcc",
-                               "v_pk_fma_f32", "v_mov_b32"};
+                               "v_pk_fma_f32", "v_mov_b32", "v_mad_u64_u32", "v_fma_f64",
+                               "v_mul_lo_u32", "v_mul_hi_u32", "v_mul_u32_u24", "v_xor_b32",
+                               "v_alignbit_b32", "v_mul_f64"};
 
 template <int M>
 static double t_mode(int W, int iters, float *out)
@@ -94,6 +106,8 @@ int main(int argc, char **argv)
     report<8>(ghz, out); report<9>(ghz, out); report<10>(ghz, out); report<11>(ghz, out);
     report<12>(ghz, out); report<13>(ghz, out); report<14>(ghz, out); report<15>(ghz, out);
     report<16>(ghz, out); report<17>(ghz, out);
+    report<18>(ghz, out); report<19>(ghz, out); report<20>(ghz, out); report<21>(ghz, out);
+    report<22>(ghz, out); report<23>(ghz, out); report<24>(ghz, out); report<25>(ghz, out);
     printf("hip: %s\n", hipGetErrorString(hipDeviceSynchronize()));
     return 0;
 }
