@@ -22,8 +22,8 @@ struct BlockPlan {
     static constexpr int E = 64, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
     static constexpr int NT = 64 * A;                      // threads per block
     static constexpr int ST = 0;                           // (R, 5)
-    static constexpr int ACT = (ST + R * 5 + 3) & ~3;      // (R, 2)
-    static constexpr int OB = (ACT + R * 2 + 3) & ~3;      // (E, O, 2)
+    static constexpr int ACTW = (ST + R * 5 + 3) & ~3;     // (A, 2, E) actions, per wave
+    static constexpr int OB = (ACTW + 2 * R + 3) & ~3;     // (E, O, 2)
     static constexpr int TG = (OB + E * O * 2 + 3) & ~3;   // (E, 2)
     static constexpr int SN = (TG + E * 2 + 3) & ~3;       // (E,)
     static constexpr int TM = (SN + E + 3) & ~3;           // (E,) bytes
@@ -44,6 +44,28 @@ __device__ __forceinline__ void block_glds(int k, int A, int w, const void *src,
                                            unsigned lane)
 {
     if (k % A == w) glds_span<NB, AUX>(src, dst, lane);
+}
+
+// LDS-DMA instructions glds_span<NB> issues (one per KiB, one for the tail)
+__host__ __device__ constexpr int glds_count(int NB)
+{
+    return (NB / 16 + 63) / 64 + ((NB % 16) / 4 > 0 ? 1 : 0);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n (0..7; larger waits for all)
+__device__ __forceinline__ void wait_vmcnt(int n)
+{
+    switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
 }
 
 // plain strided copy of n elements by the block's NT threads (partial block)
@@ -151,22 +173,36 @@ __global__ void __launch_bounds__(64 * A)
     const int ne = (int)((P - e0) < E ? (P - e0) : E);
     const bool full = ne == E;
 
-    // ---- stage the block (spans spread over the waves)
+    // ---- this wave's actions (lane l: agent w of env l) into its own LDS
+    // slots by LDS-DMA issued before the block's spans: the wave waits for
+    // them alone (vmcnt = the span instructions it issued after them) and
+    // evaluates the heading's sin/cos while the spans are still in flight,
+    // not after the stage barrier
+    float *actw = lds + BP::ACTW + 2 * E * w;  // x at [l], y at [E + l]
+    if (!OBS_ONLY && full) {
+        const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
+        __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
+    }
+    // ---- stage the block (spans spread over the waves: span k by wave k % A)
     if (full) {
         block_glds<R * 20>(0, A, w, b.states + e0 * (A * 5), st, lane);
-        if (!OBS_ONLY) block_glds<R * 8>(1, A, w, b.actions + e0 * (A * 2), lds + BP::ACT, lane);
-        block_glds<E * O * 8>(2, A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
-        block_glds<E * 8>(3, A, w, b.target + e0 * 2, lds + BP::TG, lane);
+        block_glds<E * O * 8>(1, A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
+        block_glds<E * 8>(4, A, w, b.target + e0 * 2, lds + BP::TG, lane);
         if (!OBS_ONLY) {
-            block_glds<E * 4>(4, A, w, b.step_num + e0, lds + BP::SN, lane);
+            block_glds<E * 4>(2, A, w, b.step_num + e0, lds + BP::SN, lane);
             block_glds<E>(5, A, w, b.terminates + e0, lds + BP::TM, lane);
             if (b.formation)
-                block_glds<(5 * A + 2) * 4>(6, A, w, b.formation, lds + BP::FORM, lane);
+                block_glds<(5 * A + 2) * 4>(7, A, w, b.formation, lds + BP::FORM, lane);
         }
     } else {
         const int nr = ne * A;
         block_copy(b.states + e0 * (A * 5), st, nr * 5, tid, NT);
-        if (!OBS_ONLY) block_copy(b.actions + e0 * (A * 2), lds + BP::ACT, nr * 2, tid, NT);
+        if (!OBS_ONLY && (int)lane < ne) {  // (each lane its own slots: no barrier)
+            const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
+            actw[lane] = pa[0];
+            actw[E + lane] = pa[1];
+        }
         block_copy(b.obstacles + e0 * (O * 2), lds + BP::OB, ne * O * 2, tid, NT);
         block_copy(b.target + e0 * 2, lds + BP::TG, ne * 2, tid, NT);
         if (!OBS_ONLY) {
@@ -207,6 +243,43 @@ __global__ void __launch_bounds__(64 * A)
             }
         }
     }
+    // the heading's sin/cos (environment.py:113-115, 131-137), under the
+    // remaining staging latency
+    float sn = 0.0f, c = 1.0f, a1 = 0.0f;
+    if (!OBS_ONLY) {
+        if (full) {
+            // span instructions this wave issued after its two action loads
+            constexpr int n0 = (0 % A == 0 ? glds_count(R * 20) : 0) +
+                               (1 % A == 0 ? glds_count(E * O * 8) : 0) +
+                               (4 % A == 0 ? glds_count(E * 8) : 0) +
+                               (2 % A == 0 ? glds_count(E * 4) : 0) +
+                               (5 % A == 0 ? glds_count(E) : 0);
+            constexpr int n1 = (0 % A == 1 ? glds_count(R * 20) : 0) +
+                               (1 % A == 1 ? glds_count(E * O * 8) : 0) +
+                               (4 % A == 1 ? glds_count(E * 8) : 0) +
+                               (2 % A == 1 ? glds_count(E * 4) : 0) +
+                               (5 % A == 1 ? glds_count(E) : 0);
+            constexpr int n2 = (0 % A == 2 ? glds_count(R * 20) : 0) +
+                               (1 % A == 2 ? glds_count(E * O * 8) : 0) +
+                               (4 % A == 2 ? glds_count(E * 8) : 0) +
+                               (2 % A == 2 ? glds_count(E * 4) : 0) +
+                               (5 % A == 2 ? glds_count(E) : 0);
+            constexpr int nf = glds_count((5 * A + 2) * 4);
+            static_assert(A <= 3 || (A > 3 && true), "spans 0..7 over the waves");
+            int n = w == 0 ? n0 : (w == 1 ? n1 : (w == 2 ? n2 : 0));
+            if (A > 3) n = 0;  // (more waves: wait for everything)
+            if (b.formation && 7 % A == w) n += nf;
+            wait_vmcnt(A > 3 ? 0 : n);
+        }
+        float a0 = actw[lane];
+        a1 = actw[E + lane];
+        if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
+            KArgsK *kl = kargs_late<kHotKargsOff>();
+            a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
+            a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
+        }
+        sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+    }
     const int l = (int)lane;  // env of this lane within the block
     const int r = l * A + w;  // row of this lane
     const bool row_on = l < ne;
@@ -241,15 +314,6 @@ __global__ void __launch_bounds__(64 * A)
         dy = s[3];
     }
     if (!OBS_ONLY) {
-        const float2 act = reinterpret_cast<const float2 *>(lds + BP::ACT)[r];
-        float a0 = act.x, a1 = act.y;
-        if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
-            KArgsK *kl = kargs_late<kHotKargsOff>();
-            a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
-            a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
-        }
-        float sn, c;
-        sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
         const float ndx = c * dx + (-sn) * dy;
         const float ndy = sn * dx + c * dy;
         float *s = st + 5 * r;
