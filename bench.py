@@ -23,11 +23,12 @@ barrier + synchronize; K timed steps; synchronize + barrier; the max over
 ranks. value = N*P*K / max time.
 
 roofline (the step kernel): ``launch_us`` = average duration of one step
-launch over the timed steps - HIP events on the launch stream around a second,
-untimed pass of the same K steps (the timed pass itself carries no events:
+launch over the timed steps - HIP events on the launch stream around further,
+untimed passes of the same K steps (the timed pass itself carries no events:
 recording one there adds ~13 us of GPU-side marker processing per region,
-scripts/diag/sync_overhead.py), so it includes any gap the host leaves
-between launches; ``achieved`` = algorithmic bytes per launch (read
+scripts/diag/sync_overhead.py), each started behind a short device spin so the
+region holds the K launches and any gap the host leaves between them, not the
+host's start-up gap before the first; the median of three; ``achieved`` = algorithmic bytes per launch (read
 28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at A3/O3) / ``launch_us``,
 against the 8 TB/s HBM peak. Cross-check: ``graph_replay_launch_us``, the
 same launches back to back from a hipGraph of a second Env of the same shape
@@ -58,6 +59,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402  (importing torch does not initialise the GPU)
 
 HBM_PEAK_GBS = 8000.0
+SPIN_CYCLES = 200_000  # ~0.1 ms of device spin (bench main: the event pass)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
@@ -356,14 +358,23 @@ def main():
     # the same K steps again with HIP events on the launch stream around
     # them: the GPU-side time per step of the timed loop (diagnostic; not
     # the value)
+    # A short device spin ahead of the start event keeps the queue busy while
+    # the host enqueues the first steps, so the region holds the K launches
+    # back to back and not the host's start-up gap before the first one
+    # (at K = 20 that gap moved launch_us by up to 1.5 us between runs on one
+    # box); three such passes, the median.
     barrier()
     torch.cuda.synchronize()
-    ev0.record()
-    for i in range(a.steps):
-        env.step(actions[(a.steps + i) % len(actions)])
-    ev1.record()
-    torch.cuda.synchronize()
-    region_us = ev0.elapsed_time(ev1) * 1e3 / a.steps
+    regions = []
+    for rep in range(3):
+        torch.cuda._sleep(SPIN_CYCLES)
+        ev0.record()
+        for i in range(a.steps):
+            env.step(actions[((2 + rep) * a.steps + i) % len(actions)])
+        ev1.record()
+        torch.cuda.synchronize()
+        regions.append(ev0.elapsed_time(ev1) * 1e3 / a.steps)
+    region_us = sorted(regions)[1]
 
     kern_us, kern_med = kernel_time_us(kenv, actions)
     del kenv
@@ -403,6 +414,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "launch_us": region_us,
+                         "launch_us_passes": regions,
                          "graph_replay_launch_us": kern_us,
                          "graph_replay_launch_us_median": kern_med,
                          "alg_bytes_per_launch": launch_bytes,

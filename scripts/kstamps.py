@@ -44,6 +44,7 @@ def main():
                 env.step(acts_l[i % 8])
             torch.cuda.synchronize()
             raw = buf.view(nb, 24).cpu().numpy().astype(np.int64)
+            gidx = np.nonzero(raw[:, 0] > 0)[0]  # stamps slot = global wave index
             raw = raw[raw[:, 0] > 0]  # waves past the last tile record nothing
             st = raw[:, :16].reshape(-1, 8, 2)
             entry = raw[:, 16] * 10.0 / 1e3
@@ -128,6 +129,25 @@ def main():
                     out[f"{prev_name}->{name}"] = round(float(np.median(t[m] - prev[m])), 3)
                     prev_name, prev = name, t
             print(cfg, "with_reobs sub-phases (median us):", out)
+            # the same per wave of the workgroup (WPB waves per workgroup:
+            # A for the env-block kernel, 4 for the pair-split kernel)
+            wpb = int(os.environ.get("WPB", str(A)))
+            wid = gidx[reo] % wpb
+            for w in range(wpb):
+                m = wid == w
+                if not m.any():
+                    continue
+                out = {}
+                prev_name, prev = seq[0]
+                for name, t in seq[1:]:
+                    mm = m & (t > 0) & (prev > 0)
+                    if mm.any():
+                        out[f"{prev_name}->{name}"] = round(float(np.median(t[mm] - prev[mm])), 3)
+                        prev_name, prev = name, t
+                print(cfg, f"with_reobs wave {w} of {wpb}: env phase",
+                      round(float(np.median(ph[reo][m, 3])), 3), "sub-phases", out,
+                      "nfin histogram", {int(k): int(v) for k, v in
+                                         zip(*np.unique(raw[reo][m, 19], return_counts=True))})
         del env
 
 
