@@ -52,22 +52,6 @@ __host__ __device__ constexpr int glds_count(int NB)
     return (NB / 16 + 63) / 64 + ((NB % 16) / 4 > 0 ? 1 : 0);
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n (0..7; larger waits for all)
-__device__ __forceinline__ void wait_vmcnt(int n)
-{
-    switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-
 // plain strided copy of n elements by the block's NT threads (partial block)
 template <class T>
 __device__ __forceinline__ void block_copy(const T *__restrict__ src, T *__restrict__ dst, int n,

@@ -409,6 +409,103 @@ __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, con
     }
 }
 
+// Native re-init and re-observation of the finished envs of many-obstacle
+// shapes (pair-split kernel, kSplitTpl) in ONE pass over the workgroup, with
+// the formation `form` and its observation template `tpl`
+// (marlnav_formation_obs) staged in LDS with the tile. Per finished env and
+// thread: the Philox block of one obstacle j (the draws native_fresh_env
+// makes; thread j < O also blends obstacle j into LDS and the global
+// obstacles), that obstacle's pairs with agents tid / O, tid / O + nt / O, ...
+// (the agents' blends computed by the item), one template pair (target or
+// other agent: copied, with the distance cap) and at most one blend of the
+// state or target (LDS; the global target). The items run concurrently:
+// blend_in is idempotent, so an item that reads a value another item already
+// blended gets the same bits. The template pairs hold only when every agent
+// coordinate and the target blend to the formation's bits; a blend item that
+// finds otherwise (a non-finite old value) sets `unclean`, and the caller then
+// recomputes every pair (reobs_block) after the barrier that ends this pass.
+// NT threads (all of the workgroup's), a multiple of O: a thread's pairs are
+// compile-time unrolled, so their chains interleave.
+template <int A, int O, int NT, class Envs, class List>
+__device__ __forceinline__ void reinit_reobs_tpl(KArgsK *kl, const Envs &ev, const float *form,
+                                                 const float2 *__restrict__ tpl, const List &list,
+                                                 int nfin, float cap, int tid, int *unclean)
+{
+    static_assert(NT % O == 0, "whole obstacle columns per pass");
+    constexpr int agd = NT / O;
+    float *gob = kl->a.b.obstacles;
+    float *gtg = kl->a.b.target;
+    const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
+    const int64_t eoff = kl->a.env_offset;
+    const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
+    const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
+    const int j = tid % O, ag0 = tid / O;
+    for (int fe = 0; fe < nfin; ++fe) {
+        const int c = list[fe];
+        const int64_t e = ev.env(c);
+        // obstacle j: its Philox block (obstacles 2jb, 2jb + 1) and blend
+        float v[4];
+        native_obst_draws(seed, sidx, (uint64_t)(eoff + e), j >> 1, rx, mx, ry, my, v);
+        const float *oo = ev.obst(c) + 2 * j;
+        const float px = blend_in(oo[0], (j & 1) ? v[2] : v[0]);
+        const float py = blend_in(oo[1], (j & 1) ? v[3] : v[1]);
+        // its pairs with agents ag0, ag0 + agd, ... (per wave and agent: the
+        // short sqrt / division sequences when every coordinate passes
+        // coord_ok, IEEE otherwise)
+#pragma unroll
+        for (int k = 0; k * agd < A; ++k) {
+            const int ag = ag0 + k * agd;
+            const bool on = ag < A;
+            const float *s = form + 5 * (on ? ag : 0), *so = ev.state(c) + 5 * (on ? ag : 0);
+            const float ox = blend_in(so[0], s[0]), oy = blend_in(so[1], s[1]);
+            const float dx = blend_in(so[2], s[2]), dy = blend_in(so[3], s[3]);
+            const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+            bool unused = true;
+            float d, ang;
+            if (__ballot(on && !cok) == 0ull) {
+                d = pair_dist<true>(ox, oy, px, py, unused);
+                ang = pair_angle<true>(ox, oy, px, py, dx, dy, d, cap, unused);
+            } else {
+                d = pair_dist<false>(ox, oy, px, py, unused);
+                ang = pair_angle<false>(ox, oy, px, py, dx, dy, d, cap, unused);
+            }
+            if (on) {
+                float *o = ev.row(c, ag);
+                o[2 + j] = ang;
+                o[2 + O + j] = d;
+            }
+        }
+        if (ag0 == 0) {  // (after this thread's own reads of the old obstacle)
+            float *ow = ev.obst(c) + 2 * j;
+            ow[0] = px;
+            ow[1] = py;
+            out_el(gob, e * O * 2 + 2 * j, px);
+            out_el(gob, e * O * 2 + 2 * j + 1, py);
+        }
+        // template pairs: m = 0 the target, m >= 1 other agent m - 1
+#pragma unroll
+        for (int p = tid; p < A * A; p += NT) {
+            const int ag = p / A, m = p - ag * A;
+            const float2 t = tpl[p];
+            const int sa = m == 0 ? 0 : 2 + 2 * O + (m - 1);
+            const int sd = m == 0 ? 1 : 2 + 2 * O + (A - 1) + (m - 1);
+            float *o = ev.row(c, ag);
+            o[sa] = t.y < cap ? 0.0f : t.x;  // the cap (environment.py:172-177)
+            o[sd] = t.y;
+        }
+        // blends of the state and target (environment.py:76-90)
+        for (int k2 = tid; k2 < 5 * A + 2; k2 += NT) {
+            const bool tg = k2 >= 5 * A;
+            float *d = tg ? ev.targ(c) + (k2 - 5 * A) : ev.state(c) + k2;
+            const float vb = blend_in(*d, form[k2]);
+            *d = vb;
+            if (tg) out_el(gtg, 2 * e + (k2 - 5 * A), vb);
+            if ((tg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(form[k2]))
+                *unclean = 1;
+        }
+    }
+}
+
 // The finished envs of a block as a wave-uniform ballot mask (env code = bit
 // position; the env-block kernel): entry fe is the fe-th set bit, found by
 // scalar bit scans over the few entries one pass of items touches - no LDS

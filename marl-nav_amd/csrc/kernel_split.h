@@ -92,6 +92,11 @@ constexpr bool kSplitSpread = A * (1 + O + (A - 1)) >= 32;
 template <int A, int O>
 constexpr bool kSplitTpl = kSplitSpread<A, O> && O > 8;
 
+// ... re-initialised and re-observed in one pass (reinit_reobs_tpl: the
+// workgroup's threads cover whole obstacle columns)
+template <int A, int O>
+constexpr bool kSplitTplPass = kSplitTpl<A, O> && (64 * kWavesPerBlock) % O == 0;
+
 // Extra LDS cycles of the workgroup-spread row-reward read (kernel_split.h,
 // wave 0, lane = tile cw * R + row rw, reading the row's K bond terms at
 // tile base cw * F + BOND, row stride K, one ds_read_b32 per term): banks are
@@ -167,9 +172,9 @@ struct SplitPlan {
     // the workgroup's per-env inputs, parked for wave 0's per-env phase)
     static constexpr int ENVIN = (kWavesPerBlock * (1 + EPW) + 1 + 3) & ~3;
     static constexpr int FTP = (ENVIN + 2 * kWavesPerBlock * EPW + 3) & ~3;
-    // then (kSplitSpread shapes, native re-init) the fresh obstacle draws of
-    // the workgroup's EW envs, component k of obstacle j of env code c at
-    // PRE + (2j + k) * EW + c (kernel_reinit.h native_obst_draws)
+    // then (kSplitSpread shapes with O <= 8, native re-init) the fresh
+    // obstacle draws of the workgroup's EW envs, component k of obstacle j of
+    // env code c at PRE + (2j + k) * EW + c (kernel_reinit.h native_obst_draws)
     static constexpr int EW = kWavesPerBlock * EPW;
     static constexpr int PRE = (FTP + (kSplitTpl<A, O> ? NCP : 0) + 3) & ~3;
     static constexpr int BLK = PRE + (kSplitSpread<A, O> && O <= 8 ? 2 * O * EW : 0);
@@ -408,8 +413,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     const MarlnavParams pr = load_params(K);
     const bool wt = (pr.flags & kWriteThroughFlag) != 0;  // written-through outputs
     float *const pre = lds + kWavesPerBlock * SP::FLOATS + SP::PRE;
+    // the workgroup's live waves (the waves past the last tile have exited)
+    const int64_t blk0 = (int64_t)blockIdx.x * kWavesPerBlock;
+    const int live = (int)(K->a.ntiles - blk0 < kWavesPerBlock ? K->a.ntiles - blk0
+                                                              : kWavesPerBlock);
     // (the fused native re-init of few-obstacle shapes only: at A16/O32 the
-    // draws cost the stage more than they save, 4096x16x32 12.62 -> 12.76 us)
+    // draws cost the stage ~1 us, more than they save in the tail)
     constexpr bool kPre = kSplitSpread<A, O> && O <= 8;
     if constexpr (kPre && !NOISY && !OBS_ONLY) {
         // native re-init: this wave's envs' fresh obstacles (Philox draws of
@@ -430,7 +439,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                                       pr.obs_range_y, pr.obs_mean_y, v);
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        if (2 * jb + k / 2 < O) pre[(4 * jb + k) * SP::EW + wib * EPW + cl] = v[k];
+                        if (2 * jb + k / 2 < O)
+                            pre[(4 * jb + k) * SP::EW + wib * EPW + cl] = v[k];
                 }
             }
         }
@@ -443,6 +453,28 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
     wave_sync();
     STAMP(1);
+
+    // kSplitTpl (native re-init): the formation and its observation template
+    // (NCP floats) into registers now, a few per thread, so their loads run
+    // under the move and observe phases; every workgroup parks them in its
+    // FTP region before the per-env barrier, for the one-pass re-init /
+    // re-observation of finished envs (reinit_reobs_tpl). (Loaded after the
+    // stage wait: no LDS-DMA is pending, so no LDS read waits for them.)
+    constexpr int KCP = (SP::NCP + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock);
+    float cp[KCP];
+    bool tpl_on = false;
+    if constexpr (kSplitTpl<A, O> && !NOISY && !OBS_ONLY) {
+        KArgsK *kl = kargs_late<kHotKargsOff>();
+        const float *cfo = kl->a.b.formation, *ctp = kl->a.b.formation_obs;
+        tpl_on = cfo && ctp && !kl->a.b.fresh_states;
+        if (tpl_on) {
+#pragma unroll
+            for (int k2 = 0; k2 < KCP; ++k2) {
+                const int idx = (int)threadIdx.x + k2 * 64 * kWavesPerBlock;
+                if (idx < SP::NCP) cp[k2] = idx < SP::NF ? cfo[idx] : ctp[idx - SP::NF];
+            }
+        }
+    }
 
     // ---- _move_agents (environment.py:113-123): every lane of a row moves
     // it (same instructions either way), the row leader stores it
@@ -549,7 +581,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     t.ta = orow[0];  // computed by lane LPR-1 (wave_sync above)
                     t.td = orow[1];
                 }
-                if constexpr (kSplitSpread<A, O>) {
+                if constexpr (kSplitSpread<A, O> && !MARLNAV_SPLIT_RR_LEADER) {
                     // the row's reduced terms; wave 0 finishes every row of
                     // the workgroup after the barrier (row_reward)
                     reinterpret_cast<float4 *>(wl + SP::RED)[row] =
@@ -562,26 +594,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         }
     }
     STAMP(3);
-
-    // formation + template (kSplitTpl, native re-init) into registers now,
-    // so their load latency hides behind the per-env phase; a block that
-    // finds finished envs parks them in LDS for reinit_block /
-    // reobs_block_tpl
-    constexpr int KCP = (SP::NCP + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock);
-    float cp[KCP];
-    bool tpl_on = false;
-    if constexpr (kSplitTpl<A, O> && !NOISY && !OBS_ONLY) {
-        KArgsK *kl = kargs_late<kHotKargsOff>();
-        const float *cfo = kl->a.b.formation, *ctp = kl->a.b.formation_obs;
-        tpl_on = ctp && !kl->a.b.fresh_states;
-        if (tpl_on) {
-#pragma unroll
-            for (int k2 = 0; k2 < KCP; ++k2) {
-                const int idx = (int)threadIdx.x + k2 * 64 * kWavesPerBlock;
-                if (idx < SP::NCP) cp[k2] = idx < SP::NF ? cfo[idx] : ctp[idx - SP::NF];
-            }
-        }
-    }
 
     if (!OBS_ONLY) {
         wave_sync();
@@ -669,20 +681,25 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             float *bsn = reinterpret_cast<float *>(bcnt) + SP::ENVIN;
             unsigned *bterm = reinterpret_cast<unsigned *>(bsn + kWavesPerBlock * EPW);
             if (threadIdx.x == 0) *unclean = 0;
+            if (tpl_on) {  // (uniform: every wave holds its part)
+                float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
+#pragma unroll
+                for (int k2 = 0; k2 < KCP; ++k2) {
+                    const int idx = (int)threadIdx.x + k2 * 64 * kWavesPerBlock;
+                    if (idx < SP::NCP) ftp[idx] = cp[k2];
+                }
+            }
             if (env_on) {
                 bsn[wib * EPW + (int)lane] = sn_in;
                 bterm[wib * EPW + (int)lane] = term_in;
             }
-            const int64_t blk0 = (int64_t)blockIdx.x * kWavesPerBlock;
-            const int live = (int)(K->a.ntiles - blk0 < kWavesPerBlock ? K->a.ntiles - blk0
-                                                                      : kWavesPerBlock);
             __syncthreads();
             STAMP(4);
             if (wib == 0) {
                 // every row of the workgroup: its reward terms (one lane per
                 // row, all 64 lanes busy where the row leaders were 1 in LPR)
                 static_assert(kWavesPerBlock * R <= 64, "one lane per row of the workgroup");
-                if ((int)lane < live * R) {
+                if (!MARLNAV_SPLIT_RR_LEADER && (int)lane < live * R) {
                     const int cw = (int)lane / R, rw = (int)lane - cw * R;
                     float *wlc = lds + cw * SP::FLOATS;
                     float4 *rp = reinterpret_cast<float4 *>(wlc + SP::RED) + rw;
@@ -731,40 +748,30 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
                     reinit_reobs_native<A, O, SP::EW>(kl, ev, kl->a.b.formation, list, nfin,
                                                       pr.cap_distance, tid, nt, pre);
-                } else if (kSplitTpl<A, O> && tpl_on) {
-                    // formation + template to LDS (from the registers when all
-                    // the block's waves are live, else straight from global)
-                    float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
-                    if (live == kWavesPerBlock) {
-#pragma unroll
-                        for (int k2 = 0; k2 < KCP; ++k2) {
-                            const int idx = tid + k2 * 64 * kWavesPerBlock;
-                            if (idx < SP::NCP) ftp[idx] = cp[k2];
+                    __syncthreads();
+                } else if (kSplitTplPass<A, O> && tpl_on && live == kWavesPerBlock) {
+                    if constexpr (kSplitTplPass<A, O>) {
+                        // one pass (formation and template parked by every wave)
+                        const float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
+                        reinit_reobs_tpl<A, O, 64 * kWavesPerBlock>(
+                            kl, ev, ftp, reinterpret_cast<const float2 *>(ftp + SP::NF), list,
+                            nfin, pr.cap_distance, tid, unclean);
+                        __syncthreads();
+                        STAMPX(3);
+                        if (*unclean) {  // an agent or target off the formation: every pair
+                            reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
+                            __syncthreads();
                         }
-                    } else {
-                        for (int idx = tid; idx < SP::NCP; idx += nt)
-                            ftp[idx] = idx < SP::NF ? kl->a.b.formation[idx]
-                                                    : kl->a.b.formation_obs[idx - SP::NF];
                     }
-                    __syncthreads();
-                    reinit_block<A, O>(kl, ev, ftp, list, nfin, tid, nt, unclean);
-                    __syncthreads();
-                    STAMPX(3);
-                    if (*unclean == 0)
-                        reobs_block_tpl<A, O>(ev, list, nfin, pr.cap_distance,
-                                              reinterpret_cast<const float2 *>(ftp + SP::NF),
-                                              tid, nt);
-                    else
-                        reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
                 } else {
                     if (!NOISY) {
-                        reinit_block<A, O, kPre ? SP::EW : 0>(kl, ev, kl->a.b.formation, list, nfin,
-                                                              tid, nt, nullptr, pre);
+                        reinit_block<A, O, kPre ? SP::EW : 0>(
+                            kl, ev, kl->a.b.formation, list, nfin, tid, nt, nullptr, pre);
                         __syncthreads();
                     }
                     reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
+                    __syncthreads();
                 }
-                __syncthreads();
             }
         } else {
             bool fin = false;
