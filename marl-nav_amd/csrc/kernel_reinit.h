@@ -443,6 +443,29 @@ __device__ __forceinline__ void reinit_reobs_tpl(KArgsK *kl, const Envs &ev, con
     for (int fe = 0; fe < nfin; ++fe) {
         const int c = list[fe];
         const int64_t e = ev.env(c);
+        // (the template copies and blends first: their LDS round trips run
+        // under the Philox chain that follows)
+        // template pairs: m = 0 the target, m >= 1 other agent m - 1
+#pragma unroll
+        for (int p = tid; p < A * A; p += NT) {
+            const int ag = p / A, m = p - ag * A;
+            const float2 t = tpl[p];
+            const int sa = m == 0 ? 0 : 2 + 2 * O + (m - 1);
+            const int sd = m == 0 ? 1 : 2 + 2 * O + (A - 1) + (m - 1);
+            float *o = ev.row(c, ag);
+            o[sa] = t.y < cap ? 0.0f : t.x;  // the cap (environment.py:172-177)
+            o[sd] = t.y;
+        }
+        // blends of the state and target (environment.py:76-90)
+        for (int k2 = tid; k2 < 5 * A + 2; k2 += NT) {
+            const bool tg = k2 >= 5 * A;
+            float *d = tg ? ev.targ(c) + (k2 - 5 * A) : ev.state(c) + k2;
+            const float vb = blend_in(*d, form[k2]);
+            *d = vb;
+            if (tg) out_el(gtg, 2 * e + (k2 - 5 * A), vb);
+            if ((tg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(form[k2]))
+                *unclean = 1;
+        }
         // obstacle j: its Philox block (obstacles 2jb, 2jb + 1) and blend
         float v[4];
         native_obst_draws(seed, sidx, (uint64_t)(eoff + e), j >> 1, rx, mx, ry, my, v);
@@ -481,27 +504,6 @@ __device__ __forceinline__ void reinit_reobs_tpl(KArgsK *kl, const Envs &ev, con
             ow[1] = py;
             out_el(gob, e * O * 2 + 2 * j, px);
             out_el(gob, e * O * 2 + 2 * j + 1, py);
-        }
-        // template pairs: m = 0 the target, m >= 1 other agent m - 1
-#pragma unroll
-        for (int p = tid; p < A * A; p += NT) {
-            const int ag = p / A, m = p - ag * A;
-            const float2 t = tpl[p];
-            const int sa = m == 0 ? 0 : 2 + 2 * O + (m - 1);
-            const int sd = m == 0 ? 1 : 2 + 2 * O + (A - 1) + (m - 1);
-            float *o = ev.row(c, ag);
-            o[sa] = t.y < cap ? 0.0f : t.x;  // the cap (environment.py:172-177)
-            o[sd] = t.y;
-        }
-        // blends of the state and target (environment.py:76-90)
-        for (int k2 = tid; k2 < 5 * A + 2; k2 += NT) {
-            const bool tg = k2 >= 5 * A;
-            float *d = tg ? ev.targ(c) + (k2 - 5 * A) : ev.state(c) + k2;
-            const float vb = blend_in(*d, form[k2]);
-            *d = vb;
-            if (tg) out_el(gtg, 2 * e + (k2 - 5 * A), vb);
-            if ((tg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(form[k2]))
-                *unclean = 1;
         }
     }
 }

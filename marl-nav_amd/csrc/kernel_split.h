@@ -92,6 +92,15 @@ constexpr bool kSplitSpread = A * (1 + O + (A - 1)) >= 32;
 template <int A, int O>
 constexpr bool kSplitTpl = kSplitSpread<A, O> && O > 8;
 
+// Where the per-row reward terms are finished: on each row's leader lane at
+// the end of the pair phase (few-obstacle shapes: 1024x3x8 5.09 -> 5.00 us,
+// A/B in profiles/r03_ab_logs2.txt), or, for the workgroup-spread
+// many-obstacle shapes, on wave 0 after the per-env barrier, one lane per row
+// (4096x16x32 11.76 vs 11.84 us on the row leaders). MARLNAV_SPLIT_RR_LEADER
+// (A/B builds) forces the row leaders everywhere.
+template <int A, int O>
+constexpr bool kSplitRRLeader = !kSplitSpread<A, O> || O <= 8 || MARLNAV_SPLIT_RR_LEADER;
+
 // ... re-initialised and re-observed in one pass (reinit_reobs_tpl: the
 // workgroup's threads cover whole obstacle columns)
 template <int A, int O>
@@ -581,7 +590,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     t.ta = orow[0];  // computed by lane LPR-1 (wave_sync above)
                     t.td = orow[1];
                 }
-                if constexpr (kSplitSpread<A, O> && !MARLNAV_SPLIT_RR_LEADER) {
+                if constexpr (kSplitSpread<A, O> && !kSplitRRLeader<A, O>) {
                     // the row's reduced terms; wave 0 finishes every row of
                     // the workgroup after the barrier (row_reward)
                     reinterpret_cast<float4 *>(wl + SP::RED)[row] =
@@ -699,7 +708,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 // every row of the workgroup: its reward terms (one lane per
                 // row, all 64 lanes busy where the row leaders were 1 in LPR)
                 static_assert(kWavesPerBlock * R <= 64, "one lane per row of the workgroup");
-                if (!MARLNAV_SPLIT_RR_LEADER && (int)lane < live * R) {
+                if (!kSplitRRLeader<A, O> && (int)lane < live * R) {
                     const int cw = (int)lane / R, rw = (int)lane - cw * R;
                     float *wlc = lds + cw * SP::FLOATS;
                     float4 *rp = reinterpret_cast<float4 *>(wlc + SP::RED) + rw;

@@ -42,9 +42,8 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_AB
 #define MARLNAV_AB 0
 #endif
-// A/B variant (not timing-only): the split kernel's workgroup-spread shapes
-// finish each row's reward on its row leader (as the per-wave shapes do)
-// instead of on wave 0 after the per-env barrier
+// A/B variant (not timing-only): every workgroup-spread shape of the split
+// kernel finishes each row's reward on its row leader (kSplitRRLeader)
 #ifndef MARLNAV_SPLIT_RR_LEADER
 #define MARLNAV_SPLIT_RR_LEADER 0
 #endif
