@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 3: GPU tests of the working tree, then a same-box A/B of
-# libmarlnav.so against $LIBS at $CFGS (graph replay, steady mix).
+# GPU tests of the working tree (TESTS=0: none), then a same-box A/B of
+# libmarlnav.so against $LIBS at $CFGS (graph replay, steady mix):
+#   CFGS=65536x3x3,4096x16x32 LIBS=marl-nav_amd/lib/ref.so bash scripts/ab_gpu.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
