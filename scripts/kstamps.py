@@ -120,7 +120,9 @@ def main():
             x = raw[reo][:, 20:24] * 10.0 / 1e3
             t3 = rt[reo][:, 3]
             t5 = rt[reo][:, 5]
-            seq = [("observed", t3)] + [(f"x{k}", x[:, k]) for k in range(4)] + [("reobs_end", t5)]
+            # XORDER: the order the X slots are reached in (default 0,1,2,3)
+            xo = [int(v) for v in os.environ.get("XORDER", "0,1,2,3").split(",")]
+            seq = [("observed", t3)] + [(f"x{k}", x[:, k]) for k in xo] + [("reobs_end", t5)]
             out = {}
             prev_name, prev = seq[0]
             for name, t in seq[1:]:
