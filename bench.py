@@ -22,22 +22,23 @@ clocks, which at the driver's 20-step setting was the difference between
 barrier + synchronize; K timed steps; synchronize + barrier; the max over
 ranks. value = N*P*K / max time.
 
-roofline (the step kernel): ``launch_us`` = average duration of one step
-launch over the timed steps - HIP events on the launch stream around further,
-untimed passes of the same K steps (the timed pass itself carries no events:
-recording one there adds ~13 us of GPU-side marker processing per region,
-scripts/diag/sync_overhead.py), each started behind a short device spin so the
-region holds the K launches and any gap the host leaves between them, not the
-host's start-up gap before the first; the median of three; ``achieved`` = algorithmic bytes per launch (read
-28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at A3/O3) / ``launch_us``,
-against the 8 TB/s HBM peak. Cross-check: ``graph_replay_launch_us``, the
+roofline (the step kernel): ``launch_us`` = the timed region's time per step
+(= ``ms_per_step``; one launch per step, the region's fixed synchronisation
+cost included, so ``frac`` is a lower bound that agrees with a rocprofv3
+average of the same launches); ``achieved`` = algorithmic bytes per launch
+(read 28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at A3/O3) /
+``launch_us``, against the 8 TB/s HBM peak. Beside it: ``event_launch_us``,
+HIP events on the launch stream around further, untimed passes of the same K
+steps (the timed pass itself carries no events: recording one there adds
+~13 us of GPU-side marker processing per region, scripts/diag/sync_overhead.py),
+each started behind a short device spin; the median of three. Cross-check: ``graph_replay_launch_us``, the
 same launches back to back from a hipGraph of a second Env of the same shape
 (the timed env's state and counters untouched), which is what a rocprofv3
 kernel duration of back-to-back launches measures. ``traffic``: HBM bytes per
 launch from the committed rocprofv3 PMC summary for this config (profiles/;
 not measured in this run - the source is named), or null.
 
-cpu_baseline (rank 0, N=1): oracle/torch_ref.py - the reference's step
+cpu_baseline (rank 0, every N; after the timed region): oracle/torch_ref.py - the reference's step
 restated with its own execution structure in eager PyTorch (pinned bit for
 bit to the reference's golden vectors, tests/test_torch_ref.py) - timed on
 the host CPU with all available cores and with one thread on a bounded
@@ -297,6 +298,15 @@ def load_traffic(path, workload):
     return ent.get("hbm_bytes_per_launch"), ent.get("source", os.path.relpath(path, ROOT))
 
 
+def default_backend():
+    """torch.distributed backend of the N>1 harness: gloo unless
+    MARLNAV_BENCH_BACKEND says otherwise."""
+    b = os.environ.get("MARLNAV_BENCH_BACKEND", "gloo")
+    if b not in ("gloo", "nccl"):
+        raise SystemExit(f"MARLNAV_BENCH_BACKEND={b!r}: gloo or nccl")
+    return b
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -306,9 +316,12 @@ def main():
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {a.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # MARLNAV_BENCH_BACKEND=gloo rehearses the N>1 path on fewer GPUs than
-    # ranks (ranks share devices; reductions on the host)
-    backend = os.environ.get("MARLNAV_BENCH_BACKEND", "nccl")
+    # The N>1 harness (barriers, the max-over-ranks time, summed counters,
+    # the gathered slice table) runs over gloo on the host by default: the
+    # data path has no collective, so no RCCL is needed.
+    # MARLNAV_BENCH_BACKEND=nccl opts into RCCL. Under gloo, ranks beyond the
+    # visible GPUs share them (a rehearsal of N ranks on fewer GPUs).
+    backend = default_backend()
     local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
@@ -354,6 +367,7 @@ def main():
     dt = time.perf_counter() - t0
     dt = pkg.shard.max_over_ranks(dt, red_dev)
     counters = pkg.shard.sum_over_ranks([env._num_trunc, env._num_col, env._num_tar], red_dev)
+    slices = pkg.shard.gather_slices(env._env_offset, P)
 
     # the same K steps again with HIP events on the launch stream around
     # them: the GPU-side time per step of the timed loop (diagnostic; not
@@ -380,13 +394,17 @@ def main():
     del kenv
     per_env = alg_bytes_per_env(A, O)
     launch_bytes = per_env * P
-    # the step kernel's average launch duration over the timed steps (HIP
-    # events on the launch stream; includes any inter-launch gap)
-    achieved = launch_bytes / (region_us * 1e-6) / 1e9
+    # roofline.achieved: algorithmic bytes per launch over the timed region's
+    # time per step (one launch per step; this includes the region's fixed
+    # synchronisation cost, so it is a lower bound on the kernel's own rate
+    # and agrees with a rocprofv3 average of the same launches). The event
+    # and graph-replay figures are kept beside it.
+    step_us = dt * 1e6 / a.steps
+    achieved = launch_bytes / (step_us * 1e-6) / 1e9
     traffic, traffic_src = load_traffic(a.pmc, f"P{P}_A{A}_O{O}")
 
     cpu = None
-    want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and world == 1)
+    want_cpu = a.cpu_baseline in ("on", "auto")
     if rank == 0 and want_cpu:
         cpu = cpu_baseline(P, A, O, a.cpu_seconds, device)
 
@@ -413,8 +431,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "launch_us": region_us,
-                         "launch_us_passes": regions,
+                         "launch_us": step_us,
+                         "launch_us_source": "timed region (ms_per_step)",
+                         "event_launch_us": region_us,
+                         "event_launch_us_passes": regions,
                          "graph_replay_launch_us": kern_us,
                          "graph_replay_launch_us_median": kern_med,
                          "alg_bytes_per_launch": launch_bytes,
@@ -422,6 +442,8 @@ def main():
             "cpu_baseline": cpu,
             "prewarm": {"seconds": a.prewarm, "scratch_env_steps": prewarm_steps},
             "episode_counters": counters,
+            "ranks": [{"rank": r, "env_offset": off, "envs": n} for r, off, n in slices],
+            "dist_backend": backend if world > 1 else None,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

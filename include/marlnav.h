@@ -133,7 +133,10 @@ typedef struct MarlnavStepBuffers {
      * step reads `states` and writes every env's new state row here, so the
      * launch never writes the lines it read (a host double-buffers the two,
      * as the reference rebinds `states` each step, environment.py:80).
-     * Must not overlap `states`. */
+     * Must not overlap `states`. The env-block and pair-split kernels write
+     * it with 16-byte vector stores and are chosen only when it is 16-byte
+     * aligned (as `states` must be for them); otherwise the step falls back
+     * to the generic wave kernel. */
     float *states_out;       /* (P, A, 5)                                  */
 } MarlnavStepBuffers;
 

@@ -24,22 +24,34 @@ constexpr bool kNtOther = false;  // per-env scalars and the wave kernel
 typedef float v4f_t __attribute__((ext_vector_type(4)));
 typedef float v2f_t __attribute__((ext_vector_type(2)));
 
+// Every output pointer is a device (global) allocation: cast it to address
+// space 1 so the stores are `global_store_*`, not `flat_store_*`. A FLAT
+// store counts on LGKM_CNT as well as VM_CNT, so the `s_waitcnt lgkmcnt(0)`
+// that a block barrier needs for the wave's LDS writes would also wait for
+// the store to leave; a global store counts on VM_CNT only.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T *gptr(T *p)
+{
+    return (__attribute__((address_space(1))) T *)p;
+}
+
 template <bool NT = kNtOther, class T>
 __device__ __forceinline__ void out_st(T *p, T v)
 {
     if constexpr (NT)
-        __builtin_nontemporal_store(v, p);
+        __builtin_nontemporal_store(v, gptr(p));
     else
-        *p = v;
+        *gptr(p) = v;
 }
 
 template <bool NT = kNtOther>
 __device__ __forceinline__ void out_st4(float *p, float4 v)
 {
+    auto *q = gptr(reinterpret_cast<v4f_t *>(p));
     if constexpr (NT)
-        __builtin_nontemporal_store(v4f_t{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f_t *>(p));
+        __builtin_nontemporal_store(v4f_t{v.x, v.y, v.z, v.w}, q);
     else
-        *reinterpret_cast<float4 *>(p) = v;
+        *q = v4f_t{v.x, v.y, v.z, v.w};
 }
 
 // ---------------------------------------------------- written-through outputs
@@ -120,10 +132,11 @@ __device__ __forceinline__ void out_el(T *arr, int64_t idx, T v)
 template <bool NT = kNtOther>
 __device__ __forceinline__ void out_st2(float *p, float2 v)
 {
+    auto *q = gptr(reinterpret_cast<v2f_t *>(p));
     if constexpr (NT)
-        __builtin_nontemporal_store(v2f_t{v.x, v.y}, reinterpret_cast<v2f_t *>(p));
+        __builtin_nontemporal_store(v2f_t{v.x, v.y}, q);
     else
-        *reinterpret_cast<float2 *>(p) = v;
+        *q = v2f_t{v.x, v.y};
 }
 
 // The pair math's FAST mode (the shortened sequences, bit-exact inside their

@@ -291,6 +291,15 @@ PyObject *do_launch(Engine *e, const void *actions, const MarlnavStepBuffers *fr
                         "that (timing runs)");
         return nullptr;
     }
+    if (capturing && e->base.states_out && e->held[kStatesAlt]) {
+        // double-buffered states swap roles on the host once per call: a
+        // capture records the swap once, so every replay would read the same
+        // buffer and write the other, and the states would never advance
+        PyErr_SetString(PyExc_RuntimeError,
+                        "Env.step under stream capture is not supported with double-buffered "
+                        "states (states_double_buffer=True): the buffer swap happens on the host");
+        return nullptr;
+    }
     OutSet *s = take_set(e, capturing);
     if (!s) return nullptr;
     MarlnavStepBuffers b = e->base;

@@ -52,6 +52,29 @@ __host__ __device__ constexpr int glds_count(int NB)
     return (NB / 16 + 63) / 64 + ((NB % 16) / 4 > 0 ? 1 : 0);
 }
 
+// The staging spans of a full block, in issue order: span id k (issued by
+// wave k % A) and its byte count. The issue sites and the per-wave vmcnt
+// that lets each wave use its own actions early both read this one table.
+template <int A, int O>
+struct BlockSpans {
+    using BP = BlockPlan<A, O>;
+    static constexpr int N = 6;
+    // states, obstacles, target, step_num, terminates (step only), formation
+    // (native re-init only)
+    static constexpr int K[N] = {0, 1, 4, 2, 5, 7};
+    static constexpr int NB[N] = {BP::R * 20, BP::E * O * 8, BP::E * 8, BP::E * 4, BP::E,
+                                  (5 * A + 2) * 4};
+    // LDS-DMA instructions wave w issues after its two action loads (the
+    // formation span counted only when `formation`)
+    static constexpr int after_actions(int w, bool formation)
+    {
+        int n = 0;
+        for (int i = 0; i < N; ++i)
+            if (K[i] % A == w && (i != N - 1 || formation)) n += glds_count(NB[i]);
+        return n;
+    }
+};
+
 // plain strided copy of n elements by the block's NT threads (partial block)
 template <class T>
 __device__ __forceinline__ void block_copy(const T *__restrict__ src, T *__restrict__ dst, int n,
@@ -169,15 +192,19 @@ __global__ void __launch_bounds__(64 * A)
         __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
     }
     // ---- stage the block (spans spread over the waves: span k by wave k % A)
+    using BS = BlockSpans<A, O>;
+    static_assert(BS::NB[0] == R * 20 && BS::NB[1] == E * O * 8 && BS::NB[2] == E * 8 &&
+                      BS::NB[3] == E * 4 && BS::NB[4] == E && BS::NB[5] == (5 * A + 2) * 4,
+                  "span table and LDS plan agree");
     if (full) {
-        block_glds<R * 20>(0, A, w, b.states + e0 * (A * 5), st, lane);
-        block_glds<E * O * 8>(1, A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
-        block_glds<E * 8>(4, A, w, b.target + e0 * 2, lds + BP::TG, lane);
+        block_glds<BS::NB[0]>(BS::K[0], A, w, b.states + e0 * (A * 5), st, lane);
+        block_glds<BS::NB[1]>(BS::K[1], A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
+        block_glds<BS::NB[2]>(BS::K[2], A, w, b.target + e0 * 2, lds + BP::TG, lane);
         if (!OBS_ONLY) {
-            block_glds<E * 4>(2, A, w, b.step_num + e0, lds + BP::SN, lane);
-            block_glds<E>(5, A, w, b.terminates + e0, lds + BP::TM, lane);
+            block_glds<BS::NB[3]>(BS::K[3], A, w, b.step_num + e0, lds + BP::SN, lane);
+            block_glds<BS::NB[4]>(BS::K[4], A, w, b.terminates + e0, lds + BP::TM, lane);
             if (b.formation)
-                block_glds<(5 * A + 2) * 4>(7, A, w, b.formation, lds + BP::FORM, lane);
+                block_glds<BS::NB[5]>(BS::K[5], A, w, b.formation, lds + BP::FORM, lane);
         }
     } else {
         const int nr = ne * A;
@@ -233,27 +260,12 @@ __global__ void __launch_bounds__(64 * A)
     if (!OBS_ONLY) {
         if (full) {
             // span instructions this wave issued after its two action loads
-            constexpr int n0 = (0 % A == 0 ? glds_count(R * 20) : 0) +
-                               (1 % A == 0 ? glds_count(E * O * 8) : 0) +
-                               (4 % A == 0 ? glds_count(E * 8) : 0) +
-                               (2 % A == 0 ? glds_count(E * 4) : 0) +
-                               (5 % A == 0 ? glds_count(E) : 0);
-            constexpr int n1 = (0 % A == 1 ? glds_count(R * 20) : 0) +
-                               (1 % A == 1 ? glds_count(E * O * 8) : 0) +
-                               (4 % A == 1 ? glds_count(E * 8) : 0) +
-                               (2 % A == 1 ? glds_count(E * 4) : 0) +
-                               (5 % A == 1 ? glds_count(E) : 0);
-            constexpr int n2 = (0 % A == 2 ? glds_count(R * 20) : 0) +
-                               (1 % A == 2 ? glds_count(E * O * 8) : 0) +
-                               (4 % A == 2 ? glds_count(E * 8) : 0) +
-                               (2 % A == 2 ? glds_count(E * 4) : 0) +
-                               (5 % A == 2 ? glds_count(E) : 0);
-            constexpr int nf = glds_count((5 * A + 2) * 4);
-            static_assert(A <= 3 || (A > 3 && true), "spans 0..7 over the waves");
-            int n = w == 0 ? n0 : (w == 1 ? n1 : (w == 2 ? n2 : 0));
-            if (A > 3) n = 0;  // (more waves: wait for everything)
-            if (b.formation && 7 % A == w) n += nf;
-            wait_vmcnt(A > 3 ? 0 : n);
+            // (BlockSpans: the same table as the issue sites above)
+            int n = 0;
+#pragma unroll
+            for (int ww = 0; ww < A; ++ww)
+                if (w == ww) n = b.formation ? BS::after_actions(ww, true) : BS::after_actions(ww, false);
+            wait_vmcnt(n);
         }
         float a0 = actw[lane];
         a1 = actw[E + lane];

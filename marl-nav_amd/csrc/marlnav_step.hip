@@ -274,7 +274,7 @@ const SplitVariant *select_split(const MarlnavDims *d, const MarlnavStepBuffers 
     if (!v->always && !force_size && pairs <= 6 && d->num_parallel >= kBlockFromEnvs)
         return nullptr;
     if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
-        !aligned(b.obs, 16))
+        !aligned(b.obs, 16) || (b.states_out && !aligned(b.states_out, 16)))
         return nullptr;
     if (!obs_only && !aligned(b.actions, 16)) return nullptr;
     return v;
@@ -329,7 +329,7 @@ const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers 
         if (x.A == d->num_agents && x.O == d->num_obstacles) v = &x;
     if (!v) return nullptr;
     if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
-        !aligned(b.obs, 16))
+        !aligned(b.obs, 16) || (b.states_out && !aligned(b.states_out, 16)))
         return nullptr;
     if (!obs_only && (!aligned(b.actions, 16) || !aligned(b.step_num, 16) ||
                       !aligned(b.terminates, 16) || (b.formation && !aligned(b.formation, 16))))
@@ -509,12 +509,12 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
     const bool noisy = !b->fresh_states && (pr->flags & MARLNAV_NOISY_AGENTS);
     const bool fsplit = g_family.load(std::memory_order_relaxed) == MARLNAV_FAMILY_SPLIT;
     if (family_allowed(MARLNAV_FAMILY_SPLIT))
-        if (const SplitVariant *v = select_split(d, *b, false, fsplit)) {
+        if (const SplitVariant *v = select_split(d, args.b, false, fsplit)) {
             g_last_family = MARLNAV_FAMILY_SPLIT;
             return launch_split(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }
     if (family_allowed(MARLNAV_FAMILY_BLOCK))
-        if (const BlockVariant *v = select_block(d, *b, false)) {
+        if (const BlockVariant *v = select_block(d, args.b, false)) {
             g_last_family = MARLNAV_FAMILY_BLOCK;
             return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }

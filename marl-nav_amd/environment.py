@@ -259,12 +259,13 @@ class Env(object):
         # the second states buffer (double-buffered states):
         # the engine's, unless replaced or of another shape
         alt = self.__dict__.pop('_states_alt_new', None)
-        if alt is None:
-            alt = eng.states_alt()
-        if alt is None or alt.shape != st.shape or alt.device != st.device:
-            alt = torch.empty_like(st)
         if not self.__dict__.get('_double_buffer', False):
-            alt = None   # in place (the default)
+            alt = None   # in place (the default): no second buffer at all
+        else:
+            if alt is None:
+                alt = eng.states_alt()
+            if alt is None or alt.shape != st.shape or alt.device != st.device:
+                alt = torch.empty_like(st)
         b = abi.MarlnavStepBuffers()
         b.states = st.data_ptr()
         b.states_out = alt.data_ptr() if alt is not None else None

@@ -2,7 +2,9 @@
 global env ids. The environment step has no exchange
 between envs, so the data path has no collective; torch.distributed is used
 only for the harness (barriers, the max-over-ranks time, summed episode
-counters), over RCCL on GPUs or gloo on CPU.
+counters, the gathered slice table). Those reductions are host-side over
+gloo by default (bench.py, MARLNAV_BENCH_BACKEND): a handful of integers and
+one float per run need no RCCL; "nccl" stays available as an opt-in.
 """
 import torch
 
@@ -40,3 +42,24 @@ def sum_over_ranks(values, device=None):
     t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [int(v) for v in t.tolist()]
+
+
+def gather_slices(env_offset, count):
+    """Every rank's (rank, env_offset, count), gathered on all ranks, in rank
+    order; rank 0 checks that all ``world`` ranks reported and that the
+    slices tile [0, sum of counts) without gaps or overlaps."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [(0, int(env_offset), int(count))]
+    world = dist.get_world_size()
+    got = [None] * world
+    dist.all_gather_object(got, (dist.get_rank(), int(env_offset), int(count)))
+    got = sorted(got)
+    if [g[0] for g in got] != list(range(world)):
+        raise RuntimeError(f"ranks reporting: {[g[0] for g in got]} of {world}")
+    end = 0
+    for r, off, n in got:
+        if off != end:
+            raise RuntimeError(f"rank {r} owns envs from {off}, expected {end}: {got}")
+        end = off + n
+    return got

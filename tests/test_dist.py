@@ -52,11 +52,12 @@ def _worker(rank, world, port, total, out_dir):
     dist.all_gather_object(gathered, (off, st, ob))
     tmax = pkg.shard.max_over_ranks(1.0 + rank)
     csum = pkg.shard.sum_over_ranks(cnt.tolist())
+    slices = pkg.shard.gather_slices(off, n)   # rank 0's check: every rank, no gaps
     if rank == 0:
         np.savez(os.path.join(out_dir, "dist.npz"),
                  st=np.concatenate([x[1] for x in sorted(gathered, key=lambda t: t[0])]),
                  ob=np.concatenate([x[2] for x in sorted(gathered, key=lambda t: t[0])]),
-                 tmax=tmax, csum=np.asarray(csum))
+                 tmax=tmax, csum=np.asarray(csum), slices=np.asarray(slices))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -69,6 +70,7 @@ def test_two_rank_shards_equal_one_batch(tmp_path, pkg):
              join=True)
     res = np.load(tmp_path / "dist.npz")
     assert float(res["tmax"]) == 2.0
+    np.testing.assert_array_equal(res["slices"], [[0, 0, 151], [1, 151, 150]])
     # single-process reference over the whole batch
     init = pkg.init_sampler(dict(pkg.set_init_params(
         pkg.default_args(num_parallel=total, num_obstacles=3), "cpu"), num_agents=3))
@@ -126,3 +128,44 @@ def test_bench_self_launches_n_ranks(monkeypatch):
     monkeypatch.setenv("LOCAL_RANK", "0")
     with pytest.raises(SystemExit):
         bench.main()
+
+
+def _gap_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import marlnav_amd as pkg
+    try:
+        pkg.shard.gather_slices(rank * 100 + (7 if rank == 1 else 0), 100)
+        msg = "no error"
+    except RuntimeError as e:
+        msg = str(e)
+    with open(os.path.join(out_dir, f"gap{rank}.txt"), "w") as fh:
+        fh.write(msg)
+    dist.destroy_process_group()
+
+
+def test_gather_slices_rejects_a_gap(tmp_path):
+    """A rank whose slice does not start where the previous one ends fails
+    the gathered-slice check on every rank (bench.py's rank-0 table)."""
+    mp.spawn(_gap_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert "rank 1 owns envs from 107, expected 100" in (tmp_path / f"gap{r}.txt").read_text()
+
+
+def test_bench_default_backend_is_gloo(monkeypatch):
+    """The N>1 harness defaults to gloo (host-side reductions, no RCCL);
+    nccl only on request; anything else is refused."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    monkeypatch.delenv("MARLNAV_BENCH_BACKEND", raising=False)
+    assert bench.default_backend() == "gloo"
+    monkeypatch.setenv("MARLNAV_BENCH_BACKEND", "nccl")
+    assert bench.default_backend() == "nccl"
+    monkeypatch.setenv("MARLNAV_BENCH_BACKEND", "mpi")
+    with pytest.raises(SystemExit):
+        bench.default_backend()

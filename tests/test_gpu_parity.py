@@ -462,6 +462,17 @@ def test_double_buffered_states(pkg, P, A, O):
             torch.cuda.synchronize()
             assert torch.equal(held, moved)   # not written by later steps
     assert len(ptrs) >= 2 and all(p != held.data_ptr() for p in [db2.states.data_ptr()])
+    # the host swaps the two buffers once per call: a captured step would
+    # replay reading one buffer and writing the other forever, so capture is
+    # refused even with allow_graph_capture
+    db2.allow_graph_capture = True
+    graph = torch.cuda.CUDAGraph()
+    scratch = torch.zeros(1, device=DEV)
+    with pytest.raises(RuntimeError, match="double-buffered"):
+        with torch.cuda.graph(graph):
+            scratch += 1   # (a non-empty capture whatever the step does)
+            db2.step(acts[0])
+    torch.cuda.synchronize()
 
 
 def test_held_states_pair_split_kernel(pkg):

@@ -142,11 +142,13 @@ def run_trace_oracle(pkg, mk, name):
     term = np.zeros(P, np.bool_)
     counters = np.zeros(3, np.int64)
     out = []
+    heads = []
     for k in range(m["steps"]):
         acts = smp().numpy()
         fs, fo, ft = (t.numpy() for t in init())
         if mock and k == 0:
             pr.flags |= pkg.abi.FRESH_STATES_FROM_MOVED
+        heads.append(np.clip(acts[..., 0], -np.pi, np.pi).astype(np.float32).ravel())
         o = orc.step(dm, pr, st, ob, tg, step_num, term, acts, fresh=(fs, fo, ft))
         if mock and k == 0:
             pr.flags &= ~pkg.abi.FRESH_STATES_FROM_MOVED
@@ -155,6 +157,7 @@ def run_trace_oracle(pkg, mk, name):
                                       o["step_num"], o["terminates"])
         counters += o["counters"]
         out.append((o, counters.copy()))
+    run_trace_oracle.heads = np.concatenate(heads)
     return m, z, out, A, O
 
 
@@ -164,6 +167,19 @@ def test_oracle_trace_matches_reference(name, pkg, mk):
     scenarios): terminations, counters, states and rewards bit for bit, obs
     within RTOL (no absolute floor)."""
     m, z, out, A, O = run_trace_oracle(pkg, mk, name)
+    # premise of the bit-exact state/reward asserts below: every heading of
+    # this trace has the reference's sin/cos (torch's CPU libm, MKL VML in
+    # this build) equal to the oracle's correctly rounded one. A new fixture
+    # or another torch libm can break it; then it fails here, by name.
+    th = run_trace_oracle.heads
+    s_ref = torch.sin(torch.from_numpy(th)).numpy()
+    c_ref = torch.cos(torch.from_numpy(th)).numpy()
+    s_orc, c_orc = orc.sincos(th)
+    bad = np.flatnonzero((s_ref.view(np.uint32) != s_orc.view(np.uint32)) |
+                         (c_ref.view(np.uint32) != c_orc.view(np.uint32)))
+    assert bad.size == 0, (f"{name}: {bad.size} headings whose torch sin/cos differ from the "
+                           f"correctly rounded value (first {th[bad[:4]]}): the bit-exact "
+                           f"state premise does not hold for this fixture / libm")
     for k, (o, c) in enumerate(out):
         where = f"{name} step {k + 1}"
         np.testing.assert_array_equal(o["terminated"], z["terminated"][k], where)
@@ -171,8 +187,7 @@ def test_oracle_trace_matches_reference(name, pkg, mk):
         np.testing.assert_array_equal(c, [z["num_trunc"][k], z["num_col"][k],
                                           z["num_tar"][k]], where)
         np.testing.assert_array_equal(o["obstacles"], z["obstacles"][k], where)
-        # every heading of these traces has MKL sin/cos equal to the
-        # correctly rounded one: states and rewards bit for bit
+        # (premise checked above) states and rewards bit for bit
         np.testing.assert_array_equal(o["states"], z["states"][k], where)
         np.testing.assert_array_equal(o["reward"], z["reward"][k], where + " reward")
         fields = orc.split_obs(o["obs"], A, O)
