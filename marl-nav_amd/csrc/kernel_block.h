@@ -396,15 +396,18 @@ __global__ void __launch_bounds__(64 * A)
 #pragma unroll
                 for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
+                if (!(MARLNAV_AB & 1024))  // (AB 1024: timing only, no per-env stores)
                 out_el(b.reward, e, rsum / (float)A);              // torch.mean (:233)
 
                 float step_num = lds[BP::SN + l] + 1.0f;           // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
                 const bool terminated = any_col || term_old;       // :213-214
+                if (!(MARLNAV_AB & 1024)) {
                 out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
                 out_el(b.terminated, e, (uint8_t)terminated);
                 out_el(b.truncated, e, (uint8_t)truncated);
+                }
                 fin = truncated || terminated;                     // :102-104
                 if (NOISY && fin) {  // noisy native re-init: serial per env
                     KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -430,6 +433,7 @@ __global__ void __launch_bounds__(64 * A)
                         out_el(kl->a.b.target, 2 * e + 1, tgl[1]);
                     }
                 }
+                if (!(MARLNAV_AB & 1024))
                 out_el(b.step_num, e, fin ? blend_in(step_num, 0.0f) : step_num);
                 tr_l = truncated;
                 co_l = any_col;
@@ -444,7 +448,7 @@ __global__ void __launch_bounds__(64 * A)
             const unsigned c_tar = __popcll(__ballot(ta_l));
             if (lane == 0) {
                 flg[0] = (int)__popcll(finmask);
-                if (c_trunc | c_col | c_tar) {
+                if ((c_trunc | c_col | c_tar) && !(MARLNAV_AB & 512)) {  // (AB 512: timing only)
                     KArgsK *kl = kargs_late<kHotKargsOff>();
                     uint64_t *cnt = kl->a.b.counters;
                     const int64_t slots = kl->a.waves;

@@ -56,6 +56,12 @@ def load():
         lib.oracle_sincos_n.restype = None
         lib.oracle_acosf_n.argtypes = [ctypes.c_int64, P, P]
         lib.oracle_acosf_n.restype = None
+        lib.oracle_acos_device_n.argtypes = [ctypes.c_int64, P, P]
+        lib.oracle_acos_device_n.restype = None
+        lib.oracle_acos_device_range.argtypes = [ctypes.c_uint32, ctypes.c_int64, P]
+        lib.oracle_acos_device_range.restype = None
+        lib.oracle_set_acos_mode.argtypes = [ctypes.c_int]
+        lib.oracle_set_acos_mode.restype = None
         lib.oracle_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P,
                                                   ctypes.c_double, P, P]
         lib.oracle_discounted_returns.restype = None
@@ -199,6 +205,42 @@ def sincos_range(first_bits, n, which=0):
     c = np.empty(n, np.float32)
     load().oracle_sincos_range(int(first_bits), int(n), int(which), _ptr(s), _ptr(c))
     return s, c
+
+
+def acos_device(x):
+    """The HIP kernel's acos (the device library's acosf, restated) over an
+    array."""
+    x = np.ascontiguousarray(x, np.float32).ravel()
+    out = np.empty_like(x)
+    load().oracle_acos_device_n(x.size, _ptr(x), _ptr(out))
+    return out
+
+
+def acos_device_range(first_bits, n):
+    """acos_device of n consecutive fp32 bit patterns from ``first_bits``."""
+    out = np.empty(n, np.float32)
+    load().oracle_acos_device_range(int(first_bits), int(n), _ptr(out))
+    return out
+
+
+ACOS_DEVICE, ACOS_GLIBC = 0, 1
+
+
+class acos_mode:
+    """Context manager / setter of the oracle's bearing acos: ACOS_DEVICE
+    (default: the HIP kernel's, so kernel and oracle agree bit for bit) or
+    ACOS_GLIBC (glibc acosf, the closest to the reference's MKL vsAcos)."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        load().oracle_set_acos_mode(int(self.mode))
+        return self
+
+    def __exit__(self, *exc):
+        load().oracle_set_acos_mode(ACOS_DEVICE)
+        return False
 
 
 def acosf_range(first_bits, n):

@@ -83,16 +83,32 @@ def _report(what, a, e, bad):
             f"got {a[tuple(i)]!r} want {e[tuple(i)]!r}")
 
 
+def assert_bits_equal(a, e, what=""):
+    """Float arrays equal bit for bit (+0 and -0 differ), except that a NaN
+    must face a NaN of any payload."""
+    a = np.ascontiguousarray(a, np.float32)
+    e = np.ascontiguousarray(e, np.float32)
+    assert a.shape == e.shape, f"{what}: shape {a.shape} vs {e.shape}"
+    an, en = np.isnan(a), np.isnan(e)
+    bad = (an != en) | (~an & (a.view(np.uint32) != e.view(np.uint32)))
+    assert not bad.any(), _report(what + " (bit-exact)", a, e, bad)
+
+
 def assert_obs_close(actual_fields, expected, prefix="obs_", rtol=RTOL, where="",
-                     exact_distances=False, angle_atol=0.0):
+                     exact_distances=False, angle_atol=0.0, exact=False):
     """The six Observations fields against expected ones: every field within
     rtol (angles with an absolute ``angle_atol`` only where a caller passes
     one), distances bit-exact with ``exact_distances`` (the oracle
     comparisons: both sides compute sqrtf(fmaf(dy,dy,dx*dx)),
-    environment.py:271-274); NaN/inf positions must match in every field."""
+    environment.py:271-274); NaN/inf positions must match in every field.
+    ``exact``: every field bit for bit (the kernel against the oracle, whose
+    bearings use the kernel's own acos, oracle/marlnav_oracle.c acos_device)."""
     for f, a in zip(OBS_FIELDS, actual_fields):
         e = expected[prefix + f] if isinstance(expected, dict) or hasattr(expected, "files") \
             else expected[f]
+        if exact:
+            assert_bits_equal(a, e, f"{where} {f}")
+            continue
         if exact_distances and f in DIST_FIELDS:
             np.testing.assert_array_equal(np.asarray(a), np.asarray(e), f"{where} {f}")
             continue

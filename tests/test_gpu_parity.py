@@ -96,9 +96,8 @@ def test_step_matches_reference_golden(pkg, name):
 
 @pytest.mark.parametrize("name", STEP_CASES)
 def test_step_bit_exact_vs_oracle(pkg, name):
-    """Same injected inputs through the oracle: dynamics, distances, flags
-    and rewards bit for bit; angles within 5e-7 relative (the device acosf vs
-    the oracle's glibc acosf, both < 1 ulp), no absolute floor."""
+    """Same injected inputs through the oracle: every output bit for bit,
+    bearings included (the oracle's acos is the kernel's, acos_device)."""
     m, z = meta(name), golden(name)
     P, A, O = m["num_parallel"], m["num_agents"], m["num_obstacles"]
     factors = {k: m[k] for k in ("risk_factor", "distance_factor", "heading_factor",
@@ -127,7 +126,7 @@ def test_step_bit_exact_vs_oracle(pkg, name):
         for f, a, e in zip(OBS_FIELDS, fg, fo):
             if "distance" in f:
                 np.testing.assert_array_equal(a, e, where + " " + f)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, exact_distances=True, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", exact=True, where=where)
         record_angle_stats("golden F1 inputs", "oracle", fg, fo)
 
 
@@ -224,7 +223,7 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
         got = np_(obs._packed)
         Oe = dm.num_obstacles
         fg, fo = orc.split_obs(got, A, Oe), orc.split_obs(exp["obs"], A, Oe)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, exact_distances=True, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", exact=True, where=where)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                "terminates"))
         tot += exp["counters"]
@@ -703,7 +702,7 @@ def test_extreme_coordinates_take_the_exact_path(pkg, P, A, O):
         got = np_(obs._packed)
         np.testing.assert_array_equal(got[..., 1], exp["obs"][..., 1], where)  # distances exact
         fg, fo = orc.split_obs(got, A, O), orc.split_obs(exp["obs"], A, O)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7, exact_distances=True, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", exact=True, where=where)
         s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))
 
@@ -738,7 +737,7 @@ def test_reference_rng_fresh_candidates_bit_exact_vs_oracle(pkg, P, A, O):
                           ("truncated", trunc), ("reward", rew)):
             np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
         fg, fo_ = orc.split_obs(np_(obs._packed), A, O), orc.split_obs(exp["obs"], A, O)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, exact_distances=True, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", exact=True, where=where)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                "terminates"))
         tot += exp["counters"].astype(np.int64)
@@ -769,7 +768,7 @@ def test_native_noisy_agents_bit_exact_vs_oracle(pkg, P, A, O):
                           ("reward", rew), ("terminated", term)):
             np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
         fg, fo_ = orc.split_obs(np_(obs._packed), A, O), orc.split_obs(exp["obs"], A, O)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7, exact_distances=True, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", exact=True, where=where)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                "terminates"))
 
@@ -790,7 +789,7 @@ def test_every_kernel_family_bit_exact_vs_oracle(pkg, P, A, O, expect):
     sizes above. Force each in turn (marlnav_debug_force_family) over the
     same seeded trajectory - native re-init, 3-step episodes, the observe-only
     instantiation through Env.observations() - and check each against the
-    oracle bit for bit (angles within the acosf budget)."""
+    oracle bit for bit."""
     ran = set()
     for fam in FAMILIES:
         g = torch.Generator().manual_seed(P + A + O)
@@ -819,8 +818,7 @@ def test_every_kernel_family_bit_exact_vs_oracle(pkg, P, A, O, expect):
                     np.testing.assert_array_equal(np_(got), exp[name], where + " " + name)
                 fg = orc.split_obs(np_(obs._packed), A, O)
                 fo = orc.split_obs(exp["obs"], A, O)
-                assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7,
-                                 exact_distances=True, where=where)
+                assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", exact=True, where=where)
                 st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target",
                                                        "step_num", "terminates"))
             ran.add(got_fam)
@@ -829,7 +827,7 @@ def test_every_kernel_family_bit_exact_vs_oracle(pkg, P, A, O, expect):
             assert lib.marlnav_debug_last_family() == got_fam
             fg = orc.split_obs(np_(o2._packed), A, O)
             assert_obs_close(fg, dict(zip(OBS_FIELDS, orc.split_obs(exp["obs"], A, O))),
-                             prefix="", rtol=5e-7, exact_distances=True, where=where + " observe")
+                             prefix="", exact=True, where=where + " observe")
         finally:
             lib.marlnav_debug_force_family(prev)
     assert ran == expect, (sorted(ran), sorted(expect))
@@ -906,8 +904,7 @@ def test_non_finite_inputs_match_oracle(pkg, P, A, O):
         got = np_(obs._packed)
         assert np.array_equal(np.isnan(got), np.isnan(exp["obs"])), where + " NaN pattern"
         fg, fo_ = orc.split_obs(got, A, O), orc.split_obs(exp["obs"], A, O)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", rtol=5e-7,
-                         exact_distances=True, where=where)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo_)), prefix="", exact=True, where=where)
         s, o, t, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))
 
@@ -945,7 +942,7 @@ def test_full_size_slices_bit_exact_vs_oracle(pkg, P, A, O):
                 np.testing.assert_array_equal(np_(got[s:s + n]), exp[name], where + " " + name)
             fg = orc.split_obs(np_(obs._packed[s:s + n]), A, O)
             assert_obs_close(fg, dict(zip(OBS_FIELDS, orc.split_obs(exp["obs"], A, O))),
-                             prefix="", rtol=5e-7, exact_distances=True, where=where)
+                             prefix="", exact=True, where=where)
             cur[i] = tuple(exp[x] for x in ("states", "obstacles", "target", "step_num",
                                             "terminates"))
 
@@ -953,7 +950,7 @@ def test_full_size_slices_bit_exact_vs_oracle(pkg, P, A, O):
 def _run_vs_oracle(env, dm, pr, st, ob, tg, sn, te, acts_list, form=None, fresh_list=None,
                    where=""):
     """Step env and the oracle side by side; every output bit for bit
-    (NaN for NaN), angles within the acosf budget. Returns the final state."""
+    (NaN for NaN). Returns the final state."""
     for k, acts in enumerate(acts_list):
         fresh = fresh_list[k] if fresh_list is not None else None
         if fresh is not None:
@@ -969,8 +966,7 @@ def _run_vs_oracle(env, dm, pr, st, ob, tg, sn, te, acts_list, form=None, fresh_
             np.testing.assert_array_equal(np_(got), exp[name], w + " " + name)
         A, O = dm.num_agents, dm.num_obstacles
         fg, fo = orc.split_obs(np_(obs._packed), A, O), orc.split_obs(exp["obs"], A, O)
-        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", rtol=5e-7,
-                         exact_distances=True, where=w)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", exact=True, where=w)
         st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
                                                 "terminates"))
     return st, ob, tg, sn, te
@@ -1048,7 +1044,7 @@ def test_cap_distance_reaches_step_and_observe(pkg, cap, shape):
     exp0 = orc.observe(dm, st, ob, tg, params=pr)
     fg = orc.split_obs(np_(env.observations()._packed), A, O)
     assert_obs_close(fg, dict(zip(OBS_FIELDS, orc.split_obs(exp0, A, O))), prefix="",
-                     rtol=5e-7, exact_distances=True, where="observe")
+                     exact=True, where="observe")
     acts = [((torch.rand(P, A, 2, generator=g) - 0.5) * 0.8).numpy() for _ in range(3)]
     _run_vs_oracle(env, dm, pr, st, ob, tg, np.zeros(P, np.float32), np.zeros(P, np.bool_),
                    acts, form=form, where=f"cap {cap}")
@@ -1125,7 +1121,7 @@ def test_configs4_sharded_slices_equal_one_batch_and_oracle(pkg):
                 np.testing.assert_array_equal(np_(got[s0:s0 + 64]), exp[name], where + name)
             fg = orc.split_obs(np_(fo._packed[s0:s0 + 64]), A, O)
             assert_obs_close(fg, dict(zip(OBS_FIELDS, orc.split_obs(exp["obs"], A, O))),
-                             prefix="", rtol=5e-7, exact_distances=True, where=where)
+                             prefix="", exact=True, where=where)
             cur[s0] = tuple(exp[x] for x in ("states", "obstacles", "target", "step_num",
                                              "terminates"))
     tot = np.sum([[e._num_trunc, e._num_col, e._num_tar] for e in shards], axis=0)

@@ -15,6 +15,18 @@ import oracle as orc
 STEP_CASES = ["step_a3o3", "step_a3o8", "step_a16o32", "step_a2o1", "step_p1"]
 
 
+@pytest.fixture(autouse=True)
+def _reference_acos():
+    """These tests pin the oracle to the reference. Its bearings use glibc's
+    acosf here, the acos closest to the reference's MKL vsAcos (96.9% of
+    uniform inputs bit-equal, against 66.6% for the HIP kernel's device
+    acosf, which is the oracle's default so that the GPU tests can compare
+    the kernel with it bit for bit; test_oracle_device_acos_vs_reference
+    checks that mode against the reference too)."""
+    with orc.acos_mode(orc.ACOS_GLIBC):
+        yield
+
+
 @pytest.fixture(scope="module")
 def mk(pkg):
     import marlnav_amd.environment as envmod
@@ -401,3 +413,44 @@ def test_oracle_replays_mappo_get_data(pkg):
     ret, (mean, std) = orc.discounted_returns(np.stack(rewards), np.stack(dones), m["gamma"])
     np.testing.assert_allclose(ret, z["returns"], rtol=1e-5, atol=1e-6)
     assert abs(mean - float(z["mean_rew"])) <= 1e-5 * abs(float(z["mean_rew"]))
+
+
+@pytest.mark.parametrize("name", STEP_CASES)
+def test_oracle_device_acos_vs_reference(name, mk):
+    """The oracle in its default mode (the HIP kernel's acos, restated:
+    acos_device) against the reference goldens: states, rewards and flags
+    exactly as in glibc mode, every observation field within RTOL with no
+    absolute floor (the device acosf is within ~1 ulp of the correctly
+    rounded acos)."""
+    m, z = meta(name), golden(name)
+    P, A, O = m["num_parallel"], m["num_agents"], m["num_obstacles"]
+    pr = mk(env_values(m))
+    dm = orc.make_dims(P, A, O)
+    for k in range(m["steps"]):
+        args = (dm, pr, z["in_states"][k], z["in_obstacles"][k], z["in_target"][k],
+                z["in_step_num"][k], z["in_terminates"][k], z["actions"][k])
+        fresh = (z["fresh_states"][k], z["fresh_obstacles"][k], z["fresh_target"][k])
+        o_glibc = orc.step(*args, fresh=fresh)
+        with orc.acos_mode(orc.ACOS_DEVICE):
+            o = orc.step(*args, fresh=fresh)
+        where = f"{name} step {k}"
+        for key in ("states", "reward", "terminated", "truncated"):
+            np.testing.assert_array_equal(o[key], o_glibc[key], where + " " + key)
+        fields = orc.split_obs(o["obs"], A, O)
+        assert_obs_close(fields, {f: z["obs_" + f][k] for f in OBS_FIELDS}, prefix="",
+                         where=where)
+        record_angle_stats("oracle F1 (device acos)", "reference", fields,
+                           [z["obs_" + f][k] for f in OBS_FIELDS])
+
+
+def test_acos_device_restatement_known_values():
+    """acos_device (the kernel's acos restated) at the branch edges and ends,
+    within 2 ulp of the correctly rounded acos and exact where the device
+    sequence is: acos(1) = 0, acos(-1) = pi rounded up, acos(0) = pi/2."""
+    x = np.array([-1.0, -0.75, -0.5000001, -0.5, -0.25, -0.0, 0.0, 0.25, 0.5, 0.5000001,
+                  0.75, 1.0, 1 - 2 ** -24, -(1 - 2 ** -24)], np.float32)
+    got = orc.acos_device(x)
+    cr = np.arccos(x.astype(np.float64)).astype(np.float32)
+    ulps = np.abs(got.view(np.int32).astype(np.int64) - cr.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 2, (x, got, cr)
+    assert got[11] == 0.0 and got[0] == np.float32(np.pi) and got[6] == np.float32(np.pi / 2)
