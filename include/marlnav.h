@@ -210,6 +210,12 @@ int marlnav_debug_force_family(int family);
  * this thread launched. */
 int marlnav_debug_last_family(void);
 
+/* Testing hook (not part of the reference's interface): the step kernels'
+ * bearing acos (environment.py:286) of the n consecutive fp32 bit patterns
+ * from `first`, into the device array out[n] (tests/golden/acos_dev_check.py
+ * compares it with the oracle's restatement over every fp32 in [-1, 1]). */
+int marlnav_debug_acos_range(uint32_t first, int64_t n, float *out, void *stream);
+
 /* Message of the last failing call on this thread. */
 const char *marlnav_last_error(void);
 

@@ -310,6 +310,59 @@ __device__ __forceinline__ void div2_fast(float x, float y, float den, float *qx
     *qy = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
 }
 
+// acos of the bearing (environment.py:286): the device library's acosf
+// sequence (ROCm ocml, as hipcc compiles it for gfx950: r = |x| > 0.5 ?
+// 0.5 - 0.5|x| : x*x, u = r * P5(r); |x| <= 0.5: pi/2 - (x + x*u);
+// |x| > 0.5: 2(s + s*u), or pi minus that for x < 0, s = sqrt(r)) written out
+// here with one change: s is the correctly rounded sqrt (sqrt_fast, exact on
+// r = 0 and on every r >= 2^-96) where the library uses v_sqrt_f32, which
+// differs from it on 9% of the r this sequence feeds it (1 520 276 of the
+// 2 130 706 434 fp32 inputs in [-1, 1] change: tests/golden/MANIFEST.json
+// "acos_device"). With every step an IEEE operation, oracle/marlnav_oracle.c
+// acos_device restates it bit for bit, so the bearings are compared with the
+// oracle exactly. MARLNAV_LIB_ACOS builds the library's acosf instead (A/B).
+#ifndef MARLNAV_LIB_ACOS
+#define MARLNAV_LIB_ACOS 0
+#endif
+__device__ __forceinline__ float acos_k(float x)
+{
+    if (MARLNAV_LIB_ACOS) return acosf(x);
+    const float ax = fabsf(x);
+    const float rt = __builtin_fmaf(ax, -0.5f, 0.5f);
+    const float x2 = x * x;
+    const bool big = ax > 0.5f;
+    const float r = big ? rt : x2;
+    float p = __builtin_fmaf(__uint_as_float(0x3d1c21a7u), r, __uint_as_float(0x3c5fc5dau));
+    p = __builtin_fmaf(r, p, __uint_as_float(0x3d034c3cu));
+    p = __builtin_fmaf(r, p, __uint_as_float(0x3d3641b1u));
+    p = __builtin_fmaf(r, p, __uint_as_float(0x3d999bc8u));
+    p = __builtin_fmaf(r, p, __uint_as_float(0x3e2aaaacu));
+    const float u = r * p;
+    bool unused = true;
+    const float sq = sqrt_fast(r, unused);
+    const float s2 = __builtin_fmaf(sq, u, sq);
+    const float zt = s2 + s2;
+    const float ztn = __uint_as_float(0x40490fdbu) - zt;                      // pi - 2 asin(sqrt r)
+    const float zs = __uint_as_float(0x3fc90fdbu) - __builtin_fmaf(x, u, x);  // pi/2 - asin(x)
+    return big ? (x < 0.0f ? ztn : zt) : zs;
+}
+
+// The bearing of a normalised difference (nx, ny) seen from heading (dirx,
+// diry): environment.py:280-286 (dot, clamp, x-residual sign, acos) and the
+// dist < cap cap (:172-177).
+template <bool FAST = false>
+__device__ __forceinline__ float bearing_of(float nx, float ny, float dirx, float diry,
+                                            float dist, float cap)
+{
+    float dot = dirx * nx + diry * ny;
+    // FAST: dot is finite, so the clamp is one v_med3 (no compare/select
+    // pairs and their VCC hazard nops); -0 passes through either way
+    dot = FAST ? __builtin_amdgcn_fmed3f(dot, -1.0f, 1.0f) : clamp_t(dot, -1.0f, 1.0f);
+    const float orth_x = nx - dot * dirx;
+    const float ang = (orth_x > 0.0f ? -1.0f : 1.0f) * acos_k(dot);
+    return dist < cap ? 0.0f : ang;
+}
+
 // _get_angles (environment.py:276-286) + the dist < 0.1 cap (:172-177).
 // FAST: shared-reciprocal division (clears ok when it may differ from IEEE).
 template <bool FAST = false>
@@ -330,13 +383,7 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
         nx = dx / den;
         ny = dy / den;
     }
-    float dot = dirx * nx + diry * ny;
-    // FAST: dot is finite, so the clamp is one v_med3 (no compare/select
-    // pairs and their VCC hazard nops); -0 passes through either way
-    dot = FAST ? __builtin_amdgcn_fmed3f(dot, -1.0f, 1.0f) : clamp_t(dot, -1.0f, 1.0f);
-    const float orth_x = nx - dot * dirx;
-    const float ang = (orth_x > 0.0f ? -1.0f : 1.0f) * acosf(dot);
-    return dist < cap ? 0.0f : ang;
+    return bearing_of<FAST>(nx, ny, dirx, diry, dist, cap);
 }
 
 // Correctly rounded fp32 sin/cos of an angle already clamped to [-pi, pi]
@@ -820,6 +867,70 @@ __device__ __forceinline__ float torch_row_sum_r(const float *x, F f)
     }
 }
 
+// _bond_reward's per-distance term (environment.py:264-269), 1 / (1 + sd^2)
+// with sd = (d - ideal) / sharpness. FAST (kTermsFastFlag set: every
+// parameter inside the short sequences' guards, FAST coordinates): the exact
+// short division and reciprocal; REFC: sharpness == 1, the division dropped.
+template <bool FAST, bool REFC = false>
+__device__ __forceinline__ float bond_term(float d, const MarlnavParams &pr, bool &ok)
+{
+    if constexpr (FAST) {
+        if constexpr (REFC) {
+            const float sd = d - pr.ideal_dist;
+            return recip_fast(1.0f + sd * sd, ok);
+        } else {
+            const DivC d_sharp = make_divc(pr.bond_sharpness, ok);
+            const float sd = div_c(d - pr.ideal_dist, d_sharp, ok);
+            return recip_fast(1.0f + sd * sd, ok);
+        }
+    } else {
+        const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
+        return 1.0f / (1.0f + sd * sd);
+    }
+}
+
+// The per-agent reward of _rews_and_terms (environment.py:184-269) for one
+// row, from its target bearing/distance, risk and collision flags, the count
+// of others in the distance band and the torch-order sum of bond terms.
+template <int A, bool FAST, bool REFC>
+__device__ __forceinline__ RowOut row_reward(float ta, float td, bool risk_any, bool col_any,
+                                             float band, float bond, const MarlnavParams &pr,
+                                             bool &ok)
+{
+    const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+    const float bandc = band < pr.max_at_prop_d ? band : pr.max_at_prop_d;
+    float dsc, soft;
+    if (FAST && (pr.flags & kTermsFastFlag)) {
+        // exact: the host set kTermsFastFlag only for parameters inside the
+        // div_c / recip_fast guards (terms_fast_params), and FAST coordinates
+        // bound every distance (coord_ok), so every operand stays in range
+        const DivC d_init = make_divc(pr.init_dist, ok);
+        soft = -1.0f * div_c(td, d_init, ok);
+        if constexpr (REFC) {
+            dsc = bandc * 0.5f;
+        } else {
+            const DivC d_mapd = make_divc(pr.max_at_prop_d, ok);
+            dsc = div_c(bandc, d_mapd, ok);
+        }
+    } else {
+        dsc = bandc / pr.max_at_prop_d;
+        soft = -1.0f * (td / pr.init_dist);
+    }
+    const float bondm = bond / (float)(A - 1);  // the bond sum can be tiny: IEEE
+    const float risk = risk_any ? 1.0f : 0.0f;
+    float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
+    float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
+    rm = rm + pr.distance_factor * dsc;
+    rh = rh + pr.distance_factor * dsc;
+    rm = rm + pr.soft_factor * soft;
+    rh = rh + pr.soft_factor * soft;
+    rm = rm + pr.bond_factor * bondm;
+    rh = rh + pr.bond_factor * bondm;
+    rm = rm - pr.risk_factor * risk;
+    rh = rh - pr.risk_factor * risk;
+    return RowOut{rm, rh, (col_any ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u)};
+}
+
 // observe_row with compile-time shape and the packed row kept in registers
 // (row[D]); others are visited as j = 0..A-2 -> agent j + (j >= a), so
 // every row index is a compile-time constant.
@@ -870,57 +981,14 @@ __device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
     }
     RowOut out{0.0f, 0.0f, 0u};
     if (TERMS) {
-        const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
-        const float ideal = pr.ideal_dist, sharp = pr.bond_sharpness;
-        const float bandc = band < pr.max_at_prop_d ? band : pr.max_at_prop_d;
-        float dsc, soft, bondm;
-        if (FAST && (pr.flags & kTermsFastFlag)) {
-            // exact: the host set kTermsFastFlag only for parameters inside
-            // the div_c / recip_fast guards (terms_fast_params), and FAST
-            // coordinates bound every distance (coord_ok), so every operand
-            // below stays in range
-            const DivC d_init = make_divc(pr.init_dist, ok);
-            soft = -1.0f * div_c(td, d_init, ok);
-            float bond;
-            if constexpr (REFC) {
-                dsc = bandc * 0.5f;
-                bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [&](float d) {
-                    const float sd = d - ideal;
-                    return recip_fast(1.0f + sd * sd, ok);
-                });
-            } else {
-                const DivC d_mapd = make_divc(pr.max_at_prop_d, ok);
-                const DivC d_sharp = make_divc(sharp, ok);
-                dsc = div_c(bandc, d_mapd, ok);
-                bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [&](float d) {
-                    const float sd = div_c(d - ideal, d_sharp, ok);
-                    return recip_fast(1.0f + sd * sd, ok);
-                });
-            }
-            bondm = bond / (float)(A - 1);  // the bond sum can be tiny: IEEE
-        } else {
-            dsc = bandc / pr.max_at_prop_d;
-            soft = -1.0f * (td / pr.init_dist);
-            const float bond = torch_row_sum_r<A - 1>(row + 2 + 2 * O + (A - 1), [ideal, sharp](float d) {
-                const float sd = (d - ideal) / sharp;
-                return 1.0f / (1.0f + sd * sd);
-            });
-            bondm = bond / (float)(A - 1);
-        }
-        const float risk = (ob_risk || ag_risk) ? 1.0f : 0.0f;
-        float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
-        float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
-        rm = rm + pr.distance_factor * dsc;
-        rh = rh + pr.distance_factor * dsc;
-        rm = rm + pr.soft_factor * soft;
-        rh = rh + pr.soft_factor * soft;
-        rm = rm + pr.bond_factor * bondm;
-        rh = rh + pr.bond_factor * bondm;
-        rm = rm - pr.risk_factor * risk;
-        rh = rh - pr.risk_factor * risk;
-        out.r_miss = rm;
-        out.r_hit = rh;
-        out.flags = ((ob_col || ag_col) ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u);
+        const float *agd = row + 2 + 2 * O + (A - 1);  // the others_distances just written
+        float bond;
+        if (FAST && (pr.flags & kTermsFastFlag))
+            bond = torch_row_sum_r<A - 1>(agd, [&](float d) { return bond_term<true, REFC>(d, pr, ok); });
+        else
+            bond = torch_row_sum_r<A - 1>(agd, [&](float d) { return bond_term<false>(d, pr, ok); });
+        out = row_reward<A, FAST, REFC>(ta, td, ob_risk || ag_risk, ob_col || ag_col, band, bond, pr,
+                                        ok);
     }
     return out;
 }

@@ -33,7 +33,8 @@ struct BlockPlan {
     static constexpr int LIST = (OBS + R * D + 3) & ~3;    // (E,) finished envs
     static constexpr int FLG = LIST + E;                   // [0] nfin, [1 + w] wave w coords bad
     static constexpr int FRESH = (FLG + 1 + A + 3) & ~3;   // (2O, E) fresh obstacle draws
-    static constexpr int FLOATS = FRESH + 2 * O * E;
+    static constexpr int PT = FRESH + 2 * O * E;           // (A, E) float2 agent-pair terms (A3)
+    static constexpr int FLOATS = PT + (A == 3 ? 2 * A * E : 0);
     static_assert(A >= 2 && A <= 16, "one wave per agent");
 };
 
@@ -139,6 +140,118 @@ __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float
         if ((k + 1) * NT <= Q2 || tid + k * NT < Q2) out_st4<kNtRows>(d2 + 4 * (tid + k * NT), v2[k]);
 }
 
+
+// LDS write of the first N floats of a register row to a row of stride D
+// floats: the widest vector the row base's alignment allows (the block's rows
+// start 16-byte aligned, so row r sits at 4*D*r bytes)
+template <int N, int D>
+__device__ __forceinline__ void lds_row_part_write(float *dst, const float *row)
+{
+    if constexpr (N % 4 == 0 && D % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < N; k += 4)
+            *reinterpret_cast<float4 *>(dst + k) = make_float4(row[k], row[k + 1], row[k + 2], row[k + 3]);
+    } else if constexpr (N % 2 == 0 && D % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < N; k += 2)
+            *reinterpret_cast<float2 *>(dst + k) = make_float2(row[k], row[k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < N; ++k) dst[k] = row[k];
+    }
+}
+
+// The observation phase of a FAST block at A = 3 with agent-pair symmetry
+// (environment.py:139-180, 184-269). The three agents of an env have three
+// unordered pairs; wave w takes pair (w, k = w + 1 mod 3) for its 64 envs and
+// computes once what both directions share: the distance (the squares of
+// +-dx are equal, so sqrtf(fmaf(dy,dy,dx*dx)) is the same bits both ways),
+// the normalised difference (div2_fast is odd in the numerator and maps +-0
+// to +0, so the reverse direction's quotient is exactly 0 - nx: no second
+// division), the bond term and the risk / collision / band flags; then the
+// two bearings (each from its own heading) go straight into both rows in LDS.
+// Each wave then observes its own row's target and obstacles. After one
+// block barrier the row's reward reads its two pairs' terms back (bond terms
+// summed in torch's order over the others in index order).
+// Every value equals what observe_row_own computes per direction; only the
+// shared work is done once (per wave: one distance, one division, one bond
+// term instead of two of each).
+template <int A, int O, bool TERMS, bool REFC>
+__device__ __forceinline__ void block_observe_sym(const float *__restrict__ st,
+                                                  const float *__restrict__ obe,
+                                                  const float *__restrict__ tge, int l, int w,
+                                                  float ox, float oy, float dirx, float diry,
+                                                  float *obs_rows, float2 *pt, float4 *red,
+                                                  const MarlnavParams &pr)
+{
+    static_assert(A == 3, "one unordered agent pair per wave");
+    constexpr int E = BlockPlan<A, O>::E, D = BlockPlan<A, O>::D, NO = 2 + 2 * O;
+    bool ok = true;  // (FAST block: every guard holds)
+    const float cap = pr.cap_distance;
+    // ---- the wave's agent pair (w, k)
+    const int k = w == A - 1 ? 0 : w + 1;
+    {
+        const float *sk = st + 5 * (A * l + k);
+        const float kx = sk[0], ky = sk[1], kdx = sk[2], kdy = sk[3];
+        const float ddx = kx - ox, ddy = ky - oy;
+        const float d = sqrt_fast(__builtin_fmaf(ddy, ddy, ddx * ddx), ok);
+        const float den = __builtin_amdgcn_fmed3f(d, 1e-12f, __builtin_inff());
+        float nx, ny;
+        div2_fast(ddx, ddy, den, &nx, &ny, ok);
+        const float a_wk = bearing_of<true>(nx, ny, dirx, diry, d, cap);
+        const float a_kw = bearing_of<true>(0.0f - nx, 0.0f - ny, kdx, kdy, d, cap);
+        // other k in row w at index k - (k > w); other w in row k at w - (w > k)
+        const int jw = k - (k > w ? 1 : 0), jk = w - (w > k ? 1 : 0);
+        float *rw = obs_rows + (A * l + w) * D + NO, *rk = obs_rows + (A * l + k) * D + NO;
+        rw[jw] = a_wk;
+        rw[(A - 1) + jw] = d;
+        rk[jk] = a_kw;
+        rk[(A - 1) + jk] = d;
+        if (TERMS) {
+            const float bt = (pr.flags & kTermsFastFlag) ? bond_term<true, REFC>(d, pr, ok)
+                                                         : bond_term<false>(d, pr, ok);
+            const unsigned fl = (d < pr.ag_risk_dist ? 1u : 0u) | (d < pr.ag_coll_dist ? 2u : 0u) |
+                                ((pr.agents_min_d < d && d < pr.agents_max_d) ? 4u : 0u);
+            pt[w * E + l] = make_float2(bt, __uint_as_float(fl));
+        }
+    }
+    // ---- own row: target and obstacles
+    float rowv[NO];
+    const float td = pair_dist<true>(ox, oy, tge[0], tge[1], ok);
+    const float ta = pair_angle<true>(ox, oy, tge[0], tge[1], dirx, diry, td, cap, ok);
+    rowv[0] = ta;
+    rowv[1] = td;
+    bool ob_risk = false, ob_col = false;
+#pragma unroll
+    for (int j = 0; j < O; ++j) {
+        const float px = obe[2 * j], py = obe[2 * j + 1];
+        const float d = pair_dist<true>(ox, oy, px, py, ok);
+        rowv[2 + j] = pair_angle<true>(ox, oy, px, py, dirx, diry, d, cap, ok);
+        rowv[2 + O + j] = d;
+        if (TERMS) {
+            ob_risk |= d < pr.ob_risk_dist;
+            ob_col |= d < pr.ob_coll_dist;
+        }
+    }
+    lds_row_part_write<NO, D>(obs_rows + (A * l + w) * D, rowv);
+    if (TERMS) {
+        __syncthreads();  // every pair's terms in LDS
+        // the others of row w in index order, and the wave that owns each pair
+        const int o0 = w == 0 ? 1 : 0, o1 = w == 2 ? 1 : 2;
+        const int p0 = o0 == k ? w : o0, p1 = o1 == k ? w : o1;
+        const float2 t0 = pt[p0 * E + l], t1 = pt[p1 * E + l];
+        const unsigned f0 = __float_as_uint(t0.y), f1 = __float_as_uint(t1.y);
+        float bt[A - 1] = {t0.x, t1.x};
+        const float bond = torch_row_sum_r<A - 1>(bt, [](float x) { return x; });
+        float band = 0.0f;
+        band += (f0 & 4u) ? 1.0f : 0.0f;
+        band += (f1 & 4u) ? 1.0f : 0.0f;
+        const RowOut ro = row_reward<A, true, REFC>(ta, td, ob_risk || ((f0 | f1) & 1u) != 0,
+                                                    ob_col || ((f0 | f1) & 2u) != 0, band, bond,
+                                                    pr, ok);
+        red[A * l + w] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
+    }
+}
 
 // Phases (one block barrier after each of the first four): stage | move +
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
@@ -347,12 +460,30 @@ __global__ void __launch_bounds__(64 * A)
     // ---- observations of the moved state + reward terms (:99-100)
     float4 *red = reinterpret_cast<float4 *>(lds + BP::RED);
     float *obs_rows = lds + BP::OBS;
-    if (row_on) {
+    // agent-pair symmetry (block_observe_sym): FAST A3 blocks; the A/B
+    // switch MARLNAV_NO_SYM keeps every block on the per-direction path
+    constexpr bool kSym = A == 3 && !MARLNAV_NO_SYM;
+    const bool refc = !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f && pr.max_at_prop_d == 2.0f;
+    bool sym = false;
+    if constexpr (kSym) {
+        if (__builtin_expect(fast, 1)) {
+            float2 *pt = reinterpret_cast<float2 *>(lds + BP::PT);
+            if (refc)
+                block_observe_sym<A, O, !OBS_ONLY, true>(st, lds + BP::OB + 2 * O * l,
+                                                         lds + BP::TG + 2 * l, l, w, ox, oy, dx, dy,
+                                                         obs_rows, pt, red, pr);
+            else
+                block_observe_sym<A, O, !OBS_ONLY, false>(st, lds + BP::OB + 2 * O * l,
+                                                          lds + BP::TG + 2 * l, l, w, ox, oy, dx, dy,
+                                                          obs_rows, pt, red, pr);
+            sym = true;
+        }
+    }
+    if (!sym && row_on) {
         float rowv[D];
         RowOut ro;
         bool unused = true;
-        if (__builtin_expect(fast, 1) && !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f &&
-            pr.max_at_prop_d == 2.0f)
+        if (__builtin_expect(fast, 1) && refc)
             ro = observe_row_own<A, O, !OBS_ONLY, true, true>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
                                                               lds + BP::TG + 2 * l, w, ox, oy, dx,
                                                               dy, rowv, pr, unused);

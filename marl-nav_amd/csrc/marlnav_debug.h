@@ -50,3 +50,8 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_AB_NOREFC
 #define MARLNAV_AB_NOREFC 0
 #endif
+// A/B variant: the env-block kernel without agent-pair symmetry (every row
+// computes both directions of its agent pairs)
+#ifndef MARLNAV_NO_SYM
+#define MARLNAV_NO_SYM 0
+#endif

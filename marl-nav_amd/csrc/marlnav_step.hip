@@ -119,6 +119,13 @@ __global__ void formation_obs_kernel(int A, const float *__restrict__ form, floa
     out[2 * i + 1] = d;
 }
 
+// marlnav_debug_acos_range: the bearing acos of consecutive fp32 patterns
+__global__ void acos_range_kernel(uint32_t first, int64_t n, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = acos_k(__uint_as_float(first + (uint32_t)i));
+}
+
 __global__ void counters_total_kernel(const uint64_t *__restrict__ c, int64_t slots,
                                       uint64_t *out3)
 {
@@ -438,6 +445,16 @@ int marlnav_debug_stamps(void *buf)
     return e == hipSuccess ? 0 : fail(MARLNAV_ELAUNCH, "stamps: %s", hipGetErrorString(e));
 }
 #endif
+
+int marlnav_debug_acos_range(uint32_t first, int64_t n, float *out, void *stream)
+{
+    if (n < 0 || (n > 0 && !out)) return fail(MARLNAV_EINVAL, "acos range: n < 0 or out NULL");
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(acos_range_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, first, n, out);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(MARLNAV_ELAUNCH, "acos range: %s", hipGetErrorString(e));
+}
 
 const char *marlnav_last_error(void) { return g_err; }
 

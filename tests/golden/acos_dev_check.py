@@ -1,17 +1,19 @@
 """The HIP kernel's acos over every fp32 in [-1, 1] (GPU box; generating script
 for tests/golden/MANIFEST.json "acos_device").
 
-The step kernels evaluate the bearing's acos (environment.py:286) with the
-device library's acosf. oracle/marlnav_oracle.c restates that function op for
-op (acos_device: the ISA's FMAs, with sqrtf for the v_sqrt_f32 it contains).
-This script runs the device function (scripts/probes/acos_lib.hip, built with
-the product's flags) over all 2 130 706 434 inputs in [-1, 1] and compares:
+The step kernels evaluate the bearing's acos (environment.py:286) with
+acos_k (marl-nav_amd/csrc/device_math.h): the device library's acosf sequence
+with the correctly rounded sqrt in place of its v_sqrt_f32.
+oracle/marlnav_oracle.c restates it op for op (acos_device). This script runs
+the kernels' acos (libmarlnav.so marlnav_debug_acos_range) and the library's
+own acosf (scripts/probes/acos_lib.hip, built with the product's flags) over
+all 2 130 706 434 inputs in [-1, 1] and compares:
 
-* device vs the oracle's restatement (must be equal on every input: this is
+* kernel vs the oracle's restatement (must be equal on every input: this is
   what lets the GPU tests compare kernel and oracle bearings bit for bit);
-* device vs MKL vsAcos (torch.acos on the host CPU: the reference's acos,
-  tests/golden/libm_check.py), vs glibc acosf and vs the correctly rounded
-  acos - how often each agrees with the reference.
+* kernel, library acosf, glibc acosf and the correctly rounded acos vs MKL
+  vsAcos (torch.acos on the host CPU: the reference's acos,
+  tests/golden/libm_check.py) - how often each agrees with the reference.
 
 usage (GPU box): python tests/golden/acos_dev_check.py [--quick] [--out FILE]
 then fold FILE into MANIFEST.json with --merge FILE (host).
@@ -48,7 +50,7 @@ def ranges(step):
     return out if step == 1 else out[::step]
 
 
-def host_counts(first, n, dev):
+def host_counts(first, n, dev, lib_acos):
     bits = (np.arange(n, dtype=np.uint64) + first).astype(np.uint32)
     x = bits.view(np.float32)
     restated = orc.acos_device_range(first, n)
@@ -58,7 +60,8 @@ def host_counts(first, n, dev):
     eq = lambda a, b: int((a.view(np.uint32) == b.view(np.uint32)).sum())  # noqa: E731
     bad = np.flatnonzero(dev.view(np.uint32) != restated.view(np.uint32))
     return (np.array([n, eq(dev, restated), eq(dev, mkl), eq(glibc, mkl), eq(cr, mkl),
-                      eq(dev, cr)], np.int64), [float(v) for v in x[bad[:4]]])
+                      eq(dev, cr), eq(lib_acos, mkl), eq(lib_acos, dev), eq(lib_acos, cr)],
+                     np.int64), [float(v) for v in x[bad[:4]]])
 
 
 def main():
@@ -79,20 +82,24 @@ def main():
             fh.write("\n")
         print("merged into", mpath)
         return
-    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "probes", "libacos.so"))
-    lib.acos_dev_range.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p,
-                                   ctypes.c_void_p]
+    import marlnav_amd as pkg
+    lib = pkg.abi.load_library()   # the step kernels' acos (marlnav_debug_acos_range)
+    libdev = ctypes.CDLL(os.path.join(ROOT, "scripts", "probes", "libacos.so"))
+    libdev.acos_dev_range.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_void_p]
     torch.set_num_threads(1)
     t0 = time.time()
-    tot = np.zeros(6, np.int64)
+    tot = np.zeros(9, np.int64)
     ex = []
     buf = torch.empty(CHUNK, dtype=torch.float32, device="cuda")
     pending = []
     with ThreadPoolExecutor(12) as pool:
         for i, (first, n) in enumerate(ranges(8 if a.quick else 1)):
-            assert lib.acos_dev_range(first, n, buf.data_ptr(), None) == 0
+            assert lib.marlnav_debug_acos_range(first, n, buf.data_ptr(), None) == 0
             dev = buf[:n].cpu().numpy()   # synchronises
-            pending.append(pool.submit(host_counts, first, n, dev))
+            assert libdev.acos_dev_range(first, n, buf.data_ptr(), None) == 0
+            lib_acos = buf[:n].cpu().numpy()
+            pending.append(pool.submit(host_counts, first, n, dev, lib_acos))
             if len(pending) >= 12:
                 c, e = pending.pop(0).result()
                 tot += c
@@ -105,15 +112,19 @@ def main():
             ex += e
     n = int(tot[0])
     res = {
-        "what": "device acosf (the step kernels' bearing acos) over every fp32 in [-1, 1], "
-                "tests/golden/acos_dev_check.py on an MI355X",
+        "what": "the step kernels' bearing acos (acos_k: the device library's acosf "
+                "sequence with the correctly rounded sqrt) and the library's own acosf "
+                "over every fp32 in [-1, 1], tests/golden/acos_dev_check.py on an MI355X",
         "inputs": n,
-        "device_equals_oracle_acos_device": int(tot[1]),
-        "device_not_equal_examples": ex[:8],
-        "device_vs_mkl": tot[2] / n,
+        "kernel_equals_oracle_acos_device": int(tot[1]),
+        "kernel_not_equal_examples": ex[:8],
+        "kernel_vs_mkl": tot[2] / n,
         "glibc_acosf_vs_mkl": tot[3] / n,
         "correctly_rounded_vs_mkl": tot[4] / n,
-        "device_vs_correctly_rounded": tot[5] / n,
+        "kernel_vs_correctly_rounded": tot[5] / n,
+        "library_acosf_vs_mkl": tot[6] / n,
+        "library_acosf_equals_kernel": int(tot[7]),
+        "library_acosf_vs_correctly_rounded": tot[8] / n,
         "seconds": round(time.time() - t0, 1),
     }
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
