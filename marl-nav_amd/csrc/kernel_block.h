@@ -17,9 +17,16 @@
 // packed observation rows are assembled in LDS and streamed out as one
 // contiguous span (a store instruction covers 1 KiB, 8 cache lines, where
 // register-row stores at a 48-byte lane stride touch 24).
-template <int A, int O>
+// LPR lanes per agent row (1, 2 or 4): E = 64 / LPR envs per block. LPR > 1
+// splits each row's pairs over LPR neighbouring lanes, for grids too small to
+// give every SIMD three waves at one lane per row (16384 envs: 256 blocks of
+// 64 leave a quarter of the SIMDs idle and each wave alone on its SIMD; at
+// LPR 4, 1024 blocks of 16 give every SIMD three waves, each with a third of
+// the pairs per lane).
+template <int A, int O, int LPR = 1>
 struct BlockPlan {
-    static constexpr int E = 64, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
+    static_assert(LPR == 1 || LPR == 2 || LPR == 4, "lanes per row: 1, 2 or 4");
+    static constexpr int E = 64 / LPR, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
     static constexpr int NT = 64 * A;                      // threads per block
     static constexpr int ST = 0;                           // (R, 5)
     static constexpr int ACTW = (ST + R * 5 + 3) & ~3;     // (A, 2, E) actions, per wave
@@ -56,9 +63,9 @@ __host__ __device__ constexpr int glds_count(int NB)
 // The staging spans of a full block, in issue order: span id k (issued by
 // wave k % A) and its byte count. The issue sites and the per-wave vmcnt
 // that lets each wave use its own actions early both read this one table.
-template <int A, int O>
+template <int A, int O, int LPR = 1>
 struct BlockSpans {
-    using BP = BlockPlan<A, O>;
+    using BP = BlockPlan<A, O, LPR>;
     static constexpr int N = 6;
     // states, obstacles, target, step_num, terminates (step only), formation
     // (native re-init only)
@@ -253,17 +260,124 @@ __device__ __forceinline__ void block_observe_sym(const float *__restrict__ st,
     }
 }
 
+// Lane (row base + K) of an LPR-lane row group (LPR 2 or 4; groups are
+// aligned within quads), read by every lane of the group: one DPP quad_perm.
+template <int LPR, int K>
+__device__ __forceinline__ float row_lane(float v)
+{
+    static_assert(LPR == 2 || LPR == 4, "row groups inside a quad");
+    constexpr int q0 = (0 & ~(LPR - 1)) + K, q1 = (1 & ~(LPR - 1)) + K;
+    constexpr int q2 = (2 & ~(LPR - 1)) + K, q3 = (3 & ~(LPR - 1)) + K;
+    constexpr int ctrl = q0 | (q1 << 2) | (q2 << 4) | (q3 << 6);
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xf, 0xf, false));
+}
+
+template <int LPR, int K>
+__device__ __forceinline__ unsigned row_lane_u(unsigned v)
+{
+    return __float_as_uint(row_lane<LPR, K>(__uint_as_float(v)));
+}
+
+// observations() of agent row `w` of one env (environment.py:139-180) with
+// the row's NP = 1 + O + (A - 1) pairs split over LPR lanes: lane `sub` takes
+// pairs sub, sub + LPR, ... (pair 0 the target, 1..O the obstacles, then the
+// other agents in index order), writes their bearings and distances into the
+// LDS row, and the row's reward terms (:184-269) are gathered onto lane
+// sub = 0 through DPP (flags ORed, band counts added - whole numbers, so in
+// any order - and the bond terms read back in the others' index order for
+// torch's sum). Lane 0's RowOut is the row's; every value is the one
+// observe_row_own computes.
+template <int A, int O, int LPR, bool TERMS, bool FAST, bool REFC>
+__device__ __forceinline__ RowOut observe_row_lpr(const float *__restrict__ sts,
+                                                  const float *__restrict__ obe,
+                                                  const float *__restrict__ tge, int w, int sub,
+                                                  float ox, float oy, float dirx, float diry,
+                                                  float *row, const MarlnavParams &pr)
+{
+    constexpr int NP = 1 + O + (A - 1), T = (NP + LPR - 1) / LPR;
+    bool ok = true;  // (FAST: the block passed the coordinate check)
+    const float cap = pr.cap_distance;
+    const bool bt_fast = FAST && (pr.flags & kTermsFastFlag);
+    float ta = 0.0f, td = 0.0f, band = 0.0f;
+    unsigned fl = 0u;  // bit0 obstacle risk, 1 obstacle collision, 2 agent risk, 3 agent collision
+    float bt[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int p = sub + LPR * t;
+        bt[t] = 0.0f;
+        if ((t + 1) * LPR <= NP || p < NP) {
+            const bool is_tg = p == 0, is_ob = p >= 1 && p <= O;
+            const int kx = p - O - 1;  // other agent index (p > O)
+            const int m = kx + (kx >= w ? 1 : 0);
+            const float *q = is_tg ? tge : (is_ob ? obe + 2 * (p - 1) : sts + 5 * m);
+            const float px = q[0], py = q[1];
+            const float d = pair_dist<FAST>(ox, oy, px, py, ok);
+            const float ang = pair_angle<FAST>(ox, oy, px, py, dirx, diry, d, cap, ok);
+            const int sa = is_tg ? 0 : (is_ob ? 1 + p : 2 + 2 * O + kx);
+            const int sd = is_tg ? 1 : (is_ob ? 1 + O + p : 2 + 2 * O + (A - 1) + kx);
+            row[sa] = ang;
+            row[sd] = d;
+            if (TERMS) {
+                if (t == 0) {  // (pair 0 is lane 0's first)
+                    ta = ang;
+                    td = d;
+                }
+                fl |= is_ob ? ((d < pr.ob_risk_dist ? 1u : 0u) | (d < pr.ob_coll_dist ? 2u : 0u)) : 0u;
+                const bool is_ag = p > O;
+                fl |= is_ag ? ((d < pr.ag_risk_dist ? 4u : 0u) | (d < pr.ag_coll_dist ? 8u : 0u)) : 0u;
+                band += (is_ag && pr.agents_min_d < d && d < pr.agents_max_d) ? 1.0f : 0.0f;
+                bt[t] = bt_fast ? bond_term<true, REFC>(d, pr, ok) : bond_term<false>(d, pr, ok);
+            }
+        }
+    }
+    RowOut out{0.0f, 0.0f, 0u};
+    if (TERMS) {
+        // flags and band counts of the row's lanes
+        unsigned fa = fl;
+        float bsum = band;
+        fa |= row_lane_u<LPR, 1>(fl);
+        bsum += row_lane<LPR, 1>(band);
+        if constexpr (LPR == 4) {
+            fa |= row_lane_u<LPR, 2>(fl) | row_lane_u<LPR, 3>(fl);
+            bsum += row_lane<LPR, 2>(band);
+            bsum += row_lane<LPR, 3>(band);
+        }
+        // the bond terms in the others' index order: other j is pair
+        // O + 1 + j, held by lane (O + 1 + j) % LPR in its slot / LPR
+        float bv[A - 1];
+#pragma unroll
+        for (int j = 0; j < A - 1; ++j) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            const int pj = O + 1 + j;
+            const int tj = pj / LPR;
+            float v = 0.0f;
+            switch (pj % LPR) {
+            case 0: v = bt[tj]; break;
+            case 1: v = row_lane<LPR, 1>(bt[tj]); break;
+            case 2: if constexpr (LPR == 4) v = row_lane<LPR, 2>(bt[tj]); break;
+            default: if constexpr (LPR == 4) v = row_lane<LPR, 3>(bt[tj]); break;
+            }
+            bv[j] = v;
+        }
+        const float bond = torch_row_sum_r<A - 1>(bv, [](float x) { return x; });
+        out = row_reward<A, FAST, REFC>(ta, td, (fa & 5u) != 0u, (fa & 10u) != 0u, bsum, bond,
+                                        pr, ok);
+    }
+    return out;
+}
+
 // Phases (one block barrier after each of the first four): stage | move +
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
 // re-init; none in most blocks) | rows and states stream out of LDS.
-template <int A, int O, bool OBS_ONLY, bool NOISY>
+template <int A, int O, bool OBS_ONLY, bool NOISY, int LPR = 1>
 __global__ void __launch_bounds__(64 * A)
     block_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
                  const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
                  int64_t h_P, KArgs k)
 {
-    using BP = BlockPlan<A, O>;
+    using BP = BlockPlan<A, O, LPR>;
     constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
     (void)k;  // read through kargs_late<kHotKargsOff>()
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -299,13 +413,13 @@ __global__ void __launch_bounds__(64 * A)
     // evaluates the heading's sin/cos while the spans are still in flight,
     // not after the stage barrier
     float *actw = lds + BP::ACTW + 2 * E * w;  // x at [l], y at [E + l]
-    if (!OBS_ONLY && full) {
+    if (!OBS_ONLY && full && (int)lane < E) {
         const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
         __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
         __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
     }
     // ---- stage the block (spans spread over the waves: span k by wave k % A)
-    using BS = BlockSpans<A, O>;
+    using BS = BlockSpans<A, O, LPR>;
     static_assert(BS::NB[0] == R * 20 && BS::NB[1] == E * O * 8 && BS::NB[2] == E * 8 &&
                       BS::NB[3] == E * 4 && BS::NB[4] == E && BS::NB[5] == (5 * A + 2) * 4,
                   "span table and LDS plan agree");
@@ -380,8 +494,8 @@ __global__ void __launch_bounds__(64 * A)
                 if (w == ww) n = b.formation ? BS::after_actions(ww, true) : BS::after_actions(ww, false);
             wait_vmcnt(n);
         }
-        float a0 = actw[lane];
-        a1 = actw[E + lane];
+        float a0 = actw[lane / LPR];  // (the LPR lanes of a row: the same agent)
+        a1 = actw[E + lane / LPR];
         if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
             KArgsK *kl = kargs_late<kHotKargsOff>();
             a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
@@ -389,8 +503,9 @@ __global__ void __launch_bounds__(64 * A)
         }
         sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
     }
-    const int l = (int)lane;  // env of this lane within the block
-    const int r = l * A + w;  // row of this lane
+    const int l = (int)lane / LPR;   // env of this lane's row within the block
+    const int sub = (int)lane % LPR;  // the lane's place in its row's lane group
+    const int r = l * A + w;          // row of this lane
     const bool row_on = l < ne;
     const int nrow = ne * A;
     int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
@@ -432,7 +547,7 @@ __global__ void __launch_bounds__(64 * A)
         oy = oy + ndy * v;
         dx = ndx;
         dy = ndy;
-        if (row_on) {
+        if (row_on && sub == 0) {
             s[0] = ox;
             s[1] = oy;
             s[2] = dx;
@@ -462,7 +577,7 @@ __global__ void __launch_bounds__(64 * A)
     float *obs_rows = lds + BP::OBS;
     // agent-pair symmetry (block_observe_sym): FAST A3 blocks; the A/B
     // switch MARLNAV_NO_SYM keeps every block on the per-direction path
-    constexpr bool kSym = A == 3 && !MARLNAV_NO_SYM;
+    constexpr bool kSym = A == 3 && LPR == 1 && !MARLNAV_NO_SYM;
     const bool refc = !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f && pr.max_at_prop_d == 2.0f;
     bool sym = false;
     if constexpr (kSym) {
@@ -478,6 +593,25 @@ __global__ void __launch_bounds__(64 * A)
                                                           obs_rows, pt, red, pr);
             sym = true;
         }
+    }
+    if constexpr (LPR > 1) {
+        if (row_on) {
+            const float *se = st + 5 * A * l, *obe = lds + BP::OB + 2 * O * l, *tge = lds + BP::TG + 2 * l;
+            float *rw = obs_rows + r * D;
+            RowOut ro;
+            if (__builtin_expect(fast, 1) && refc)
+                ro = observe_row_lpr<A, O, LPR, !OBS_ONLY, true, true>(se, obe, tge, w, sub, ox, oy,
+                                                                       dx, dy, rw, pr);
+            else if (__builtin_expect(fast, 1))
+                ro = observe_row_lpr<A, O, LPR, !OBS_ONLY, true, false>(se, obe, tge, w, sub, ox, oy,
+                                                                        dx, dy, rw, pr);
+            else
+                ro = observe_row_lpr<A, O, LPR, !OBS_ONLY, false, false>(se, obe, tge, w, sub, ox,
+                                                                         oy, dx, dy, rw, pr);
+            if (!OBS_ONLY && sub == 0)
+                red[r] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
+        }
+        sym = true;  // (done)
     }
     if (!sym && row_on) {
         float rowv[D];
@@ -508,14 +642,16 @@ __global__ void __launch_bounds__(64 * A)
         int *flg = reinterpret_cast<int *>(lds + BP::FLG);
         const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
         // ---- per-env reductions, terminal logic (wave 0, one lane per env)
+        // (env le = lane here: one lane per env, whatever LPR)
+        const int le = (int)lane;
         if (w == 0) {
-            const bool env_on = l < ne;
+            const bool env_on = le < ne;
             bool fin = false, tr_l = false, co_l = false, ta_l = false;
             if (env_on) {
-                const int64_t e = e0 + l;
+                const int64_t e = e0 + le;
                 float4 rr[A];
 #pragma unroll
-                for (int i = 0; i < A; ++i) rr[i] = red[A * l + i];
+                for (int i = 0; i < A; ++i) rr[i] = red[A * le + i];
                 unsigned any_col = 0u, all_in = 1u;
 #pragma unroll
                 for (int i = 0; i < A; ++i) {
@@ -530,9 +666,9 @@ __global__ void __launch_bounds__(64 * A)
                 if (!(MARLNAV_AB & 1024))  // (AB 1024: timing only, no per-env stores)
                 out_el(b.reward, e, rsum / (float)A);              // torch.mean (:233)
 
-                float step_num = lds[BP::SN + l] + 1.0f;           // :96
+                float step_num = lds[BP::SN + le] + 1.0f;           // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
-                const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
+                const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[le] != 0;
                 const bool terminated = any_col || term_old;       // :213-214
                 if (!(MARLNAV_AB & 1024)) {
                 out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
@@ -553,11 +689,11 @@ __global__ void __launch_bounds__(64 * A)
                         p.angle_range = kl->p.angle_range;
                         p.flags = kl->p.flags;
                         p.seed = kl->p.seed;
-                        float *obl = lds + BP::OB + 2 * O * l;
-                        float *tgl = lds + BP::TG + 2 * l;
+                        float *obl = lds + BP::OB + 2 * O * le;
+                        float *tgl = lds + BP::TG + 2 * le;
                         native_fresh_env<NOISY>(A, O, p, lds + BP::FORM,
                                                 (uint64_t)(kl->a.env_offset + e), kl->a.step_idx,
-                                                st + 5 * A * l, obl, tgl);
+                                                st + 5 * A * le, obl, tgl);
                         float *gob = kl->a.b.obstacles;
                         for (int i = 0; i < 2 * O; ++i) out_el(gob, e * O * 2 + i, obl[i]);
                         out_el(kl->a.b.target, 2 * e, tgl[0]);
@@ -573,7 +709,7 @@ __global__ void __launch_bounds__(64 * A)
             const uint64_t finmask = __ballot(fin);
             if (fin)
                 list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] = l;
+                                               __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] = le;
             const unsigned c_trunc = __popcll(__ballot(tr_l));
             const unsigned c_col = __popcll(__ballot(co_l));
             const unsigned c_tar = __popcll(__ballot(ta_l));
@@ -598,12 +734,12 @@ __global__ void __launch_bounds__(64 * A)
             // (:105) of those envs. Disjoint LDS: wave 0 reads red/SN/TM; this
             // writes the states, obstacles, target and rows of finished envs.
             bool fin = false;
-            if (l < ne) {
+            if (le < ne) {
                 unsigned any_col = 0u;
 #pragma unroll
-                for (int i = 0; i < A; ++i) any_col |= __float_as_uint(red[A * l + i].z) & 1u;
-                fin = lds[BP::SN + l] + 1.0f > pr.trunc_after || any_col != 0u ||
-                      reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
+                for (int i = 0; i < A; ++i) any_col |= __float_as_uint(red[A * le + i].z) & 1u;
+                fin = lds[BP::SN + le] + 1.0f > pr.trunc_after || any_col != 0u ||
+                      reinterpret_cast<const uint8_t *>(lds + BP::TM)[le] != 0;
             }
             const uint64_t fm = __ballot(fin);
             STAMPX(0);

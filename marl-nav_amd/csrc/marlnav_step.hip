@@ -310,30 +310,53 @@ int launch_split(const SplitVariant &v, BlockFn fn, const StepArgs &args, const 
     return 0;
 }
 
-// env-block kernels (block_kernel) for these shapes
+// env-block kernels (block_kernel) for these shapes, at LPR lanes per agent
+// row (E = 64 / LPR envs per block)
 struct BlockVariant {
-    int A, O;
+    int A, O, lpr;
     BlockFn step, obs, noisy;
     size_t lds;
 };
 
-#define MARLNAV_BLOCK_VARIANT(A, O)                                                    \
-    {A, O, block_kernel<A, O, false, false>, block_kernel<A, O, true, false>,          \
-     block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4}
+#define MARLNAV_BLOCK_VARIANT(A, O, LPR)                                               \
+    {A, O, LPR, block_kernel<A, O, false, false, LPR>, block_kernel<A, O, true, false, LPR>, \
+     block_kernel<A, O, false, true, LPR>, (size_t)BlockPlan<A, O, LPR>::FLOATS * 4}
 const BlockVariant kBlockVariants[] = {
-    MARLNAV_BLOCK_VARIANT(3, 3),
-    MARLNAV_BLOCK_VARIANT(3, 8),
-    MARLNAV_BLOCK_VARIANT(3, 1),
-    MARLNAV_BLOCK_VARIANT(2, 1),
+    MARLNAV_BLOCK_VARIANT(3, 3, 1),
+    MARLNAV_BLOCK_VARIANT(3, 3, 2),
+    MARLNAV_BLOCK_VARIANT(3, 3, 4),
+    MARLNAV_BLOCK_VARIANT(3, 8, 1),
+    MARLNAV_BLOCK_VARIANT(3, 1, 1),
+    MARLNAV_BLOCK_VARIANT(2, 1, 1),
 };
 #undef MARLNAV_BLOCK_VARIANT
+
+// Lanes per agent row for a grid of P envs: the fewest that give the chip
+// about three waves per SIMD (kBlockWavesTarget waves: 1024 SIMDs x 3), as
+// the one-lane-per-row grid of 65536 envs x 3 agents does; 1 from there up.
+// MARLNAV_BLOCK_LPR (A/B builds) forces one.
+#ifndef MARLNAV_BLOCK_LPR
+#define MARLNAV_BLOCK_LPR 0
+#endif
+constexpr int64_t kBlockWavesTarget = 3072;
+
+int block_lpr_for(int64_t P, int A)
+{
+    if (MARLNAV_BLOCK_LPR) return MARLNAV_BLOCK_LPR;
+    int lpr = 1;
+    while (lpr < 4 && (P + 64 / lpr - 1) / (64 / lpr) * A < kBlockWavesTarget) lpr *= 2;
+    return lpr;
+}
 
 const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only)
 {
     if (d->obstacle_stride != d->num_obstacles) return nullptr;
     const BlockVariant *v = nullptr;
-    for (const BlockVariant &x : kBlockVariants)
-        if (x.A == d->num_agents && x.O == d->num_obstacles) v = &x;
+    const int want = block_lpr_for(d->num_parallel, d->num_agents);
+    for (const BlockVariant &x : kBlockVariants)  // the wanted LPR, else the largest compiled below it
+        if (x.A == d->num_agents && x.O == d->num_obstacles && x.lpr <= want &&
+            (!v || x.lpr > v->lpr))
+            v = &x;
     if (!v) return nullptr;
     if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
         !aligned(b.obs, 16) || (b.states_out && !aligned(b.states_out, 16)))
@@ -350,7 +373,7 @@ int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const 
     KArgs ka;
     ka.a = args;
     ka.p = pr;
-    ka.a.W = BlockPlan<3, 3>::E;
+    ka.a.W = 64 / v.lpr;  // envs per block
     ka.a.ntiles = (args.P + ka.a.W - 1) / ka.a.W;
     // the leading arguments (kHotKargsOff, kernel_args.h): staging pointers, P
     float *h_states = args.b.states;

@@ -185,13 +185,17 @@ class _nullctx:
                                             (65536, 3, 3, 6, 25), (409600 + 27, 3, 3, 3, 25),
                                             (2 * 16384 * 32 + 5, 2, 1, 2, 25),
                                             (12000 + 7, 3, 3, 9, 4), (20480, 3, 8, 5, 2),
-                                            (1021, 16, 32, 6, 3), (1000 + 3, 3, 8, 8, 3)])
+                                            (1021, 16, 32, 6, 3), (1000 + 3, 3, 8, 8, 3),
+                                            (16384, 3, 3, 8, 3), (32768 + 5, 3, 3, 6, 4),
+                                            (8192 + 3, 3, 3, 6, 2)])
 def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
     """Native (Philox) re-init mode, many steps, random actions, short
     episodes (ep = 2, 4: whole tiles finish at once, re-observed in several
     chunks): the GPU trajectory equals the oracle's bit for bit. The ragged
     split-kernel cases end on a workgroup with fewer live waves (1021 = 255*4
-    + 1 one-env waves) and a partial tile (1003 envs, two per LPR-8 wave)."""
+    + 1 one-env waves) and a partial tile (1003 envs, two per LPR-8 wave).
+    The env-block kernel runs with 4 lanes per agent row at 16384 and 8195
+    envs (ragged last block) and with 2 at 32773 (block_lpr_for)."""
     g = torch.Generator().manual_seed(P + A + O)
     env = make_env(pkg, P, A, O, episode_len=ep, seed=99,
                    factors=dict(risk_factor=3., distance_factor=7.))
