@@ -183,13 +183,31 @@ __device__ __forceinline__ void lds_row_part_write(float *dst, const float *row)
 // Every value equals what observe_row_own computes per direction; only the
 // shared work is done once (per wave: one distance, one division, one bond
 // term instead of two of each).
-template <int A, int O, bool TERMS, bool REFC>
-__device__ __forceinline__ void block_observe_sym(const float *__restrict__ st,
+// EARLY (native, non-noisy re-init with the fresh obstacles drawn at stage
+// time): the finished envs are known right after the block barrier - every
+// collision flag of the env is in the pair terms then - so each wave
+// re-initialises and re-observes its own agent's rows of the finished envs
+// there (kernel_reinit.h native_pair_item / native_rest_item: the same items
+// and values as reinit_reobs_native), before the observation barrier,
+// instead of waves 1..A-1 doing all of it after that barrier while wave 0
+// runs the per-env phase: the per-env phase then no longer waits for it.
+struct EarlyReinit {
+    KArgsK *kl;
+    const float *form, *pre, *sn;
+    const uint8_t *tm;
+    float *ob, *tg;
+    int64_t e0;
+    int ne;
+};
+
+template <int A, int O, bool TERMS, bool REFC, bool EARLY = false>
+__device__ __forceinline__ void block_observe_sym(float *__restrict__ st,
                                                   const float *__restrict__ obe,
                                                   const float *__restrict__ tge, int l, int w,
                                                   float ox, float oy, float dirx, float diry,
                                                   float *obs_rows, float2 *pt, float4 *red,
-                                                  const MarlnavParams &pr)
+                                                  const MarlnavParams &pr,
+                                                  const EarlyReinit &er = EarlyReinit{})
 {
     static_assert(A == 3, "one unordered agent pair per wave");
     constexpr int E = BlockPlan<A, O>::E, D = BlockPlan<A, O>::D, NO = 2 + 2 * O;
@@ -197,6 +215,8 @@ __device__ __forceinline__ void block_observe_sym(const float *__restrict__ st,
     const float cap = pr.cap_distance;
     // ---- the wave's agent pair (w, k)
     const int k = w == A - 1 ? 0 : w + 1;
+    float pair_bt = 0.0f;
+    unsigned pair_fl = 0u;  // bit0 agent risk, 1 agent collision, 2 in band; 3: row w's obstacle collision
     {
         const float *sk = st + 5 * (A * l + k);
         const float kx = sk[0], ky = sk[1], kdx = sk[2], kdy = sk[3];
@@ -215,11 +235,10 @@ __device__ __forceinline__ void block_observe_sym(const float *__restrict__ st,
         rk[jk] = a_kw;
         rk[(A - 1) + jk] = d;
         if (TERMS) {
-            const float bt = (pr.flags & kTermsFastFlag) ? bond_term<true, REFC>(d, pr, ok)
-                                                         : bond_term<false>(d, pr, ok);
-            const unsigned fl = (d < pr.ag_risk_dist ? 1u : 0u) | (d < pr.ag_coll_dist ? 2u : 0u) |
-                                ((pr.agents_min_d < d && d < pr.agents_max_d) ? 4u : 0u);
-            pt[w * E + l] = make_float2(bt, __uint_as_float(fl));
+            pair_bt = (pr.flags & kTermsFastFlag) ? bond_term<true, REFC>(d, pr, ok)
+                                                  : bond_term<false>(d, pr, ok);
+            pair_fl = (d < pr.ag_risk_dist ? 1u : 0u) | (d < pr.ag_coll_dist ? 2u : 0u) |
+                      ((pr.agents_min_d < d && d < pr.agents_max_d) ? 4u : 0u);
         }
     }
     // ---- own row: target and obstacles
@@ -242,6 +261,7 @@ __device__ __forceinline__ void block_observe_sym(const float *__restrict__ st,
     }
     lds_row_part_write<NO, D>(obs_rows + (A * l + w) * D, rowv);
     if (TERMS) {
+        pt[w * E + l] = make_float2(pair_bt, __uint_as_float(pair_fl | (ob_col ? 8u : 0u)));
         __syncthreads();  // every pair's terms in LDS
         // the others of row w in index order, and the wave that owns each pair
         const int o0 = w == 0 ? 1 : 0, o1 = w == 2 ? 1 : 2;
@@ -257,6 +277,43 @@ __device__ __forceinline__ void block_observe_sym(const float *__restrict__ st,
                                                     ob_col || ((f0 | f1) & 2u) != 0, band, bond,
                                                     pr, ok);
         red[A * l + w] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
+        if constexpr (EARLY) {
+            // finished (environment.py:96-104, 213-214): truncated, reached
+            // the target last step, or any collision of the env's rows - every
+            // agent pair's collision bit and every row's obstacle bit
+            const int p2 = 3 - p0 - p1;  // the pair without agent w
+            const unsigned f2 = __float_as_uint(pt[p2 * E + l].y);
+            const unsigned fo = f0 | f1 | f2;
+            const bool fin = l < er.ne && (er.sn[l] + 1.0f > pr.trunc_after || er.tm[l] != 0 ||
+                                           (fo & 10u) != 0u);
+            const uint64_t fm = __ballot(fin);  // (the same set in every wave)
+            if (fm) {
+                // wave w: agent w's rows of the finished envs - its NP pair
+                // items and its 5 state floats; wave 0 also the target and the
+                // obstacle blocks (LDS and global)
+                using IT = NativeItems<A, O>;
+                const BlockEnvs<A, O, D> ev{st, const_cast<float *>(er.ob), er.tg, obs_rows, er.e0};
+                const int nfin = (int)__popcll(fm);
+                const int ipw = IT::NP + 5 + (w == 0 ? 2 + IT::NB : 0);
+                const int lane = (int)(threadIdx.x & 63);
+                for (int base = 0; base < nfin * ipw; base += 64) {
+                    const int i = base + lane;
+                    const bool on = i < nfin * ipw;
+                    const int ic = on ? i : 0;
+                    const int fe = ic / ipw, rem = ic - fe * ipw;
+                    const int lo = base / ipw, hi = min((base + 63) / ipw, nfin - 1);
+                    const int c = list_code(MaskList{fm}, fe, lo, hi);
+                    if (rem < IT::NP) {  // (every lane of the wave: the pair math's ballot)
+                        native_pair_item<A, O, E>(er.kl, ev, er.form, er.pre, c, w * IT::NP + rem,
+                                                  on, pr.cap_distance);
+                    } else if (on) {
+                        const int r2 = rem - IT::NP;
+                        native_rest_item<A, O, E>(er.kl, ev, er.form, er.pre, c,
+                                                  r2 < 5 ? 5 * w + r2 : 5 * A + (r2 - 5));
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -580,17 +637,36 @@ __global__ void __launch_bounds__(64 * A)
     constexpr bool kSym = A == 3 && LPR == 1 && !MARLNAV_NO_SYM;
     const bool refc = !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f && pr.max_at_prop_d == 2.0f;
     bool sym = false;
+    // finished envs re-initialised and re-observed inside the symmetric
+    // observation phase (block_observe_sym EARLY): native non-noisy re-init
+    // with the stage-time draws
+    bool early = false;
     if constexpr (kSym) {
         if (__builtin_expect(fast, 1)) {
             float2 *pt = reinterpret_cast<float2 *>(lds + BP::PT);
-            if (refc)
-                block_observe_sym<A, O, !OBS_ONLY, true>(st, lds + BP::OB + 2 * O * l,
-                                                         lds + BP::TG + 2 * l, l, w, ox, oy, dx, dy,
-                                                         obs_rows, pt, red, pr);
-            else
-                block_observe_sym<A, O, !OBS_ONLY, false>(st, lds + BP::OB + 2 * O * l,
-                                                          lds + BP::TG + 2 * l, l, w, ox, oy, dx, dy,
-                                                          obs_rows, pt, red, pr);
+            const float *obe = lds + BP::OB + 2 * O * l, *tge = lds + BP::TG + 2 * l;
+            if constexpr (!OBS_ONLY && kPre && !(MARLNAV_AB & 1) && !MARLNAV_NO_EARLY) {
+                early = overlap;
+                if (early) {
+                    const EarlyReinit er{kargs_late<kHotKargsOff>(), lds + BP::FORM, lds + BP::FRESH,
+                                         lds + BP::SN, reinterpret_cast<const uint8_t *>(lds + BP::TM),
+                                         lds + BP::OB, lds + BP::TG, e0, ne};
+                    if (refc)
+                        block_observe_sym<A, O, true, true, true>(st, obe, tge, l, w, ox, oy, dx, dy,
+                                                                  obs_rows, pt, red, pr, er);
+                    else
+                        block_observe_sym<A, O, true, false, true>(st, obe, tge, l, w, ox, oy, dx,
+                                                                   dy, obs_rows, pt, red, pr, er);
+                }
+            }
+            if (!early) {
+                if (refc)
+                    block_observe_sym<A, O, !OBS_ONLY, true>(st, obe, tge, l, w, ox, oy, dx, dy,
+                                                             obs_rows, pt, red, pr);
+                else
+                    block_observe_sym<A, O, !OBS_ONLY, false>(st, obe, tge, l, w, ox, oy, dx, dy,
+                                                              obs_rows, pt, red, pr);
+            }
             sym = true;
         }
     }
@@ -727,7 +803,7 @@ __global__ void __launch_bounds__(64 * A)
                     }
                 }
             }
-        } else if (overlap) {
+        } else if (overlap && !early) {
             // ---- waves 1..A-1, while wave 0 runs the per-env phase: the
             // finished set from the inputs wave 0 uses (red flags, step_num,
             // terminates), then the native re-init (:104) and re-observation

@@ -55,3 +55,8 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_NO_SYM
 #define MARLNAV_NO_SYM 0
 #endif
+// A/B variant: finished envs re-initialised after the observation barrier by
+// waves 1..A-1 (the round-3 flow) also in FAST symmetric blocks
+#ifndef MARLNAV_NO_EARLY
+#define MARLNAV_NO_EARLY 0
+#endif
