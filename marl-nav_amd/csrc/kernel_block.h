@@ -288,6 +288,7 @@ __device__ __forceinline__ void block_observe_sym(float *__restrict__ st,
                                            (fo & 10u) != 0u);
             const uint64_t fm = __ballot(fin);  // (the same set in every wave)
             if (fm) {
+                if (MARLNAV_TAIL_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_TAIL_PRIO);  // (A/B)
                 // wave w: agent w's rows of the finished envs - its NP pair
                 // items and its 5 state floats; wave 0 also the target and the
                 // obstacle blocks (LDS and global)

@@ -60,3 +60,8 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_NO_EARLY
 #define MARLNAV_NO_EARLY 0
 #endif
+// A/B variant: s_setprio level of the waves that re-initialise finished envs
+// (the launch's tail), 0 = none
+#ifndef MARLNAV_TAIL_PRIO
+#define MARLNAV_TAIL_PRIO 0
+#endif

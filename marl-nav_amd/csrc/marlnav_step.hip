@@ -339,10 +339,12 @@ const BlockVariant kBlockVariants[] = {
 #define MARLNAV_BLOCK_LPR 0
 #endif
 constexpr int64_t kBlockWavesTarget = 3072;
+std::atomic<int> g_block_lpr{0};  // marlnav_debug_force_block_lpr (0: automatic)
 
 int block_lpr_for(int64_t P, int A)
 {
     if (MARLNAV_BLOCK_LPR) return MARLNAV_BLOCK_LPR;
+    if (const int f = g_block_lpr.load(std::memory_order_relaxed)) return f;
     int lpr = 1;
     while (lpr < 4 && (P + 64 / lpr - 1) / (64 / lpr) * A < kBlockWavesTarget) lpr *= 2;
     return lpr;
@@ -460,6 +462,13 @@ int marlnav_debug_force_family(int family)
 }
 
 int marlnav_debug_last_family(void) { return g_last_family; }
+
+int marlnav_debug_force_block_lpr(int lpr)
+{
+    if (lpr != 0 && lpr != 1 && lpr != 2 && lpr != 4)
+        return fail(MARLNAV_EINVAL, "lanes per row %d: 0 (automatic), 1, 2 or 4", lpr);
+    return g_block_lpr.exchange(lpr, std::memory_order_relaxed);
+}
 
 #if MARLNAV_STAMPS
 int marlnav_debug_stamps(void *buf)
