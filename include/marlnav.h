@@ -216,6 +216,11 @@ int marlnav_debug_last_family(void);
  * setting. */
 int marlnav_debug_force_block_lpr(int lpr);
 
+/* Testing hook: the env-block kernel's helper wave (A3/O3 native re-init
+ * steps): -1 automatic (grids of at most 256 blocks), 0 never, 1 always.
+ * Returns the previous setting. */
+int marlnav_debug_force_helper(int on);
+
 /* Testing hook (not part of the reference's interface): the step kernels'
  * bearing acos (environment.py:286) of the n consecutive fp32 bit patterns
  * from `first`, into the device array out[n] (tests/golden/acos_dev_check.py

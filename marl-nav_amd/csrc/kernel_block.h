@@ -23,9 +23,10 @@
 // 64 leave a quarter of the SIMDs idle and each wave alone on its SIMD; at
 // LPR 4, 1024 blocks of 16 give every SIMD three waves, each with a third of
 // the pairs per lane).
-template <int A, int O, int LPR = 1>
+template <int A, int O, int LPR = 1, bool HELP = false>
 struct BlockPlan {
     static_assert(LPR == 1 || LPR == 2 || LPR == 4, "lanes per row: 1, 2 or 4");
+    static_assert(!HELP || LPR == 1, "the helper wave serves one-lane-per-row blocks");
     static constexpr int E = 64 / LPR, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
     static constexpr int NT = 64 * A;                      // threads per block
     static constexpr int ST = 0;                           // (R, 5)
@@ -41,7 +42,9 @@ struct BlockPlan {
     static constexpr int FLG = LIST + E;                   // [0] nfin, [1 + w] wave w coords bad
     static constexpr int FRESH = (FLG + 1 + A + 3) & ~3;   // (2O, E) fresh obstacle draws
     static constexpr int PT = FRESH + 2 * O * E;           // (A, E) float2 agent-pair terms (A3)
-    static constexpr int FLOATS = PT + (A == 3 ? 2 * A * E : 0);
+    // (HELP) the fresh env's agent-obstacle pairs, (E, A, 2O): bearing then distance
+    static constexpr int FR = PT + (A == 3 ? 2 * A * E : 0);
+    static constexpr int FLOATS = FR + (HELP ? 2 * O * A * E : 0);
     static_assert(A >= 2 && A <= 16, "one wave per agent");
 };
 
@@ -425,18 +428,161 @@ __device__ __forceinline__ RowOut observe_row_lpr(const float *__restrict__ sts,
     return out;
 }
 
+// ---------------------------------------------------------- helper wave
+// Grids of at most one env-block per CU (16384 envs x 3 agents: 256 blocks of
+// 3 waves, a quarter of the SIMDs idle) get a fourth wave per block on the
+// idle SIMD. While waves 0..A-1 stage, move and observe, it draws the fresh
+// obstacles of every env of the block (the native re-init's Philox draws) and
+// computes the fresh env's agent-obstacle pairs (formation agents against
+// those obstacles; agent a between the block barriers a and a+1, so it never
+// holds a barrier back). After the observation barrier it re-initialises and
+// re-observes the finished envs alone - the target and agent-agent pairs from
+// the formation template (marlnav_formation_obs), the obstacle pairs from its
+// own table - while wave 0 runs the per-env phase: the finished-env tail
+// shrinks to copies and blends, and the draws leave the main waves' stage.
+
+// fresh obstacles of env l (lane) of the block: its NB Philox blocks
+template <int O>
+__device__ __forceinline__ void helper_draws(const MarlnavParams &pr, uint64_t sidx, uint64_t gid,
+                                             float (&fo)[2 * O])
+{
+#pragma unroll
+    for (int jb = 0; jb < (O + 1) / 2; ++jb) {
+        float v[4];
+        native_obst_draws(pr.seed, sidx, gid, jb, pr.obs_range_x, pr.obs_mean_x, pr.obs_range_y,
+                          pr.obs_mean_y, v);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (2 * jb + k / 2 < O) fo[4 * jb + k] = v[k];
+    }
+}
+
+// the fresh env's pairs of formation agent a with its O fresh obstacles (the
+// values native_pair_item computes for a clean env), into fr (E, A, 2O)
+template <int A, int O>
+__device__ __forceinline__ void helper_fresh_pairs(const float *__restrict__ gform, int a,
+                                                   const float (&fo)[2 * O], float cap, float *fr,
+                                                   int l)
+{
+    const float fx = gform[5 * a], fy = gform[5 * a + 1];
+    const float fdx = gform[5 * a + 2], fdy = gform[5 * a + 3];
+    bool cok = coord_ok(fx) && coord_ok(fy);
+#pragma unroll
+    for (int j = 0; j < 2 * O; ++j) cok = cok && coord_ok(fo[j]);
+    float *o = fr + (l * A + a) * 2 * O;
+    bool unused = true;
+    if (__ballot(!cok) == 0ull) {
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+            const float d = pair_dist<true>(fx, fy, fo[2 * j], fo[2 * j + 1], unused);
+            o[j] = pair_angle<true>(fx, fy, fo[2 * j], fo[2 * j + 1], fdx, fdy, d, cap, unused);
+            o[O + j] = d;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+            const float d = pair_dist<false>(fx, fy, fo[2 * j], fo[2 * j + 1], unused);
+            o[j] = pair_angle<false>(fx, fy, fo[2 * j], fo[2 * j + 1], fdx, fdy, d, cap, unused);
+            o[O + j] = d;
+        }
+    }
+}
+
+// The helper wave's finished-env tail (environment.py:76-90, 104-105): the
+// finished set (the test wave 0's per-env phase makes), each finished env's
+// cleanliness (every blended agent coordinate, the target and the obstacles
+// equal to their fresh values, i.e. no non-finite old value: then the
+// template and the helper's pairs describe the re-initialised env), then one
+// item per (env, row, pair) - copied when clean, computed (native_pair_item)
+// otherwise - and per state float / target / obstacle block (native_rest_item).
+template <int A, int O, int E, int D>
+__device__ __forceinline__ void helper_tail(KArgsK *kl, const BlockEnvs<A, O, D> &ev,
+                                            const float *form, const float *pre, const float *fr,
+                                            const float2 *__restrict__ tpl, const float4 *red,
+                                            const float *sn, const uint8_t *tm, int ne,
+                                            const MarlnavParams &pr, int lane)
+{
+    bool fin = false;
+    if (lane < ne) {
+        unsigned any_col = 0u;
+#pragma unroll
+        for (int i = 0; i < A; ++i) any_col |= __float_as_uint(red[A * lane + i].z) & 1u;
+        fin = sn[lane] + 1.0f > pr.trunc_after || any_col != 0u || tm[lane] != 0;
+    }
+    const uint64_t fm = __ballot(fin);
+    if (!fm) return;
+    const int nfin = (int)__popcll(fm);
+    bool cl = false;
+    if (lane < nfin) {
+        const int c = list_code(MaskList{fm}, lane, 0, nfin - 1);
+        const float *s = ev.state(c);
+        cl = true;
+#pragma unroll
+        for (int a = 0; a < A; ++a)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                cl = cl && __float_as_uint(blend_in(s[5 * a + k], form[5 * a + k])) ==
+                               __float_as_uint(form[5 * a + k]);
+        const float *t = ev.targ(c);
+        cl = cl && __float_as_uint(blend_in(t[0], form[5 * A])) == __float_as_uint(form[5 * A]);
+        cl = cl && __float_as_uint(blend_in(t[1], form[5 * A + 1])) ==
+                       __float_as_uint(form[5 * A + 1]);
+        const float *ob = ev.obst(c);
+#pragma unroll
+        for (int i = 0; i < 2 * O; ++i)
+            cl = cl && __float_as_uint(blend_in(ob[i], pre[i * E + c])) ==
+                           __float_as_uint(pre[i * E + c]);
+    }
+    const uint64_t cm = __ballot(cl);  // bit fe: finished env fe is clean
+    using IT = NativeItems<A, O>;
+    constexpr int NI = IT::NPAIR + IT::NREST;
+    const float cap = pr.cap_distance;
+    for (int base = 0; base < nfin * NI; base += 64) {
+        const int i = base + lane;
+        const bool on = i < nfin * NI;
+        const int ic = on ? i : 0;
+        const int fe = ic / NI, kk = ic - fe * NI;
+        const int c = list_code(MaskList{fm}, fe, base / NI, min((base + 63) / NI, nfin - 1));
+        if (kk < IT::NPAIR) {
+            if ((cm >> fe) & 1ull) {
+                if (on) {
+                    const int ag = kk / IT::NP, p = kk - ag * IT::NP;
+                    float *o = ev.row(c, ag);
+                    if (p >= 1 && p <= O) {
+                        const float *q = fr + (c * A + ag) * 2 * O;
+                        o[1 + p] = q[p - 1];
+                        o[1 + O + p] = q[O + p - 1];
+                    } else {
+                        const int m = p == 0 ? 0 : p - O;  // template column: 0 target, 1 + other
+                        const float2 t = tpl[ag * A + m];
+                        const int sa = p == 0 ? 0 : 2 + 2 * O + (m - 1);
+                        const int sd = p == 0 ? 1 : 2 + 2 * O + (A - 1) + (m - 1);
+                        o[sa] = t.y < cap ? 0.0f : t.x;  // the cap (environment.py:172-177)
+                        o[sd] = t.y;
+                    }
+                }
+            } else {
+                native_pair_item<A, O, E>(kl, ev, form, pre, c, kk, on, cap);
+            }
+        } else if (on) {
+            native_rest_item<A, O, E>(kl, ev, form, pre, c, kk - IT::NPAIR);
+        }
+    }
+}
+
 // Phases (one block barrier after each of the first four): stage | move +
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
 // re-init; none in most blocks) | rows and states stream out of LDS.
-template <int A, int O, bool OBS_ONLY, bool NOISY, int LPR = 1>
-__global__ void __launch_bounds__(64 * A)
+template <int A, int O, bool OBS_ONLY, bool NOISY, int LPR = 1, bool HELP = false>
+__global__ void __launch_bounds__(64 * (A + HELP))
     block_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
                  const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
                  int64_t h_P, KArgs k)
 {
-    using BP = BlockPlan<A, O, LPR>;
-    constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
+    using BP = BlockPlan<A, O, LPR, HELP>;
+    static_assert(!HELP || (!OBS_ONLY && !NOISY), "the helper serves the native re-init step");
+    constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT + (HELP ? 64 : 0);
     (void)k;  // read through kargs_late<kHotKargsOff>()
     extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS
@@ -446,8 +592,9 @@ __global__ void __launch_bounds__(64 * A)
     const int tid = (int)threadIdx.x;
     const unsigned lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // agent of this wave
+    const bool hw = HELP && w == A;  // the helper wave (no agent)
     const int64_t blk = blockIdx.x;
-    const int64_t gw = blk * A + w;  // stamps slot
+    const int64_t gw = blk * (A + HELP) + w;  // stamps slot
     KArgsK *K = kargs_late<kHotKargsOff>();
     const int64_t P = h_P;
     // launch_block's grid is exactly ntiles blocks: no exit test. The staging
@@ -471,7 +618,7 @@ __global__ void __launch_bounds__(64 * A)
     // evaluates the heading's sin/cos while the spans are still in flight,
     // not after the stage barrier
     float *actw = lds + BP::ACTW + 2 * E * w;  // x at [l], y at [E + l]
-    if (!OBS_ONLY && full && (int)lane < E) {
+    if (!OBS_ONLY && full && (int)lane < E && !hw) {
         const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
         __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
         __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
@@ -494,7 +641,7 @@ __global__ void __launch_bounds__(64 * A)
     } else {
         const int nr = ne * A;
         block_copy(b.states + e0 * (A * 5), st, nr * 5, tid, NT);
-        if (!OBS_ONLY && (int)lane < ne) {  // (each lane its own slots: no barrier)
+        if (!OBS_ONLY && (int)lane < ne && !hw) {  // (each lane its own slots: no barrier)
             const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
             actw[lane] = pa[0];
             actw[E + lane] = pa[1];
@@ -515,7 +662,22 @@ __global__ void __launch_bounds__(64 * A)
     // (one Philox block per thread at most: at A3/O8 the two passes cost the
     // stage phase more than they save, 131072x3x8 18.4 -> 19.0 us)
     constexpr bool kPre = E * ((O + 1) / 2) <= NT;
-    if (kPre && overlap && !(MARLNAV_AB & 256)) {  // (AB 256: timing only, no draws)
+    // (HELP: the helper wave's fresh obstacles of env `lane`, kept in
+    // registers from the draws until its agent-obstacle pairs are done)
+    float hfo[HELP ? 2 * O : 1];
+    (void)hfo;
+    if constexpr (HELP) {
+        if (hw && overlap) {
+            KArgsK *kl = kargs_late<kHotKargsOff>();
+            float(&fo)[2 * O] = reinterpret_cast<float(&)[2 * O]>(hfo);
+            helper_draws<O>(pr, kl->a.step_idx, (uint64_t)(kl->a.env_offset + e0 + lane), fo);
+            float *pre = lds + BP::FRESH;
+#pragma unroll
+            for (int i = 0; i < 2 * O; ++i)
+                if ((int)lane < ne) pre[i * E + lane] = fo[i];
+            helper_fresh_pairs<A, O>(b.formation, 0, fo, pr.cap_distance, lds + BP::FR, (int)lane);
+        }
+    } else if (kPre && overlap && !(MARLNAV_AB & 256)) {  // (AB 256: timing only, no draws)
         // the fresh obstacles of every env of the block (its Philox draws
         // depend only on seed, step and env id), drawn while the staging
         // loads are in flight: a finished env's re-init then reads them
@@ -542,7 +704,7 @@ __global__ void __launch_bounds__(64 * A)
     // the heading's sin/cos (environment.py:113-115, 131-137), under the
     // remaining staging latency
     float sn = 0.0f, c = 1.0f, a1 = 0.0f;
-    if (!OBS_ONLY) {
+    if (!OBS_ONLY && !hw) {
         if (full) {
             // span instructions this wave issued after its two action loads
             // (BlockSpans: the same table as the issue sites above)
@@ -563,8 +725,8 @@ __global__ void __launch_bounds__(64 * A)
     }
     const int l = (int)lane / LPR;   // env of this lane's row within the block
     const int sub = (int)lane % LPR;  // the lane's place in its row's lane group
-    const int r = l * A + w;          // row of this lane
-    const bool row_on = l < ne;
+    const int r = l * A + (hw ? 0 : w);  // row of this lane (the helper has none)
+    const bool row_on = l < ne && !hw;
     const int nrow = ne * A;
     int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
     if (tid == 0) *bad_word = 0;
@@ -617,7 +779,12 @@ __global__ void __launch_bounds__(64 * A)
     // reciprocal division (equal to IEEE there) when every coordinate of the
     // block (obstacles and targets above, moved agents here) passes coord_ok,
     // IEEE otherwise
-    if (full) {
+    if constexpr (HELP) {  // agent 1's fresh pairs, between the stage and move barriers
+        if (hw && overlap && A > 1)
+            helper_fresh_pairs<A, O>(b.formation, 1, reinterpret_cast<float(&)[2 * O]>(hfo),
+                                     pr.cap_distance, lds + BP::FR, (int)lane);
+    }
+    if (full && !hw) {
         crange.add(ox);
         crange.add(oy);
         // one word for the block, written only by waves that found one (all
@@ -635,7 +802,7 @@ __global__ void __launch_bounds__(64 * A)
     float *obs_rows = lds + BP::OBS;
     // agent-pair symmetry (block_observe_sym): FAST A3 blocks; the A/B
     // switch MARLNAV_NO_SYM keeps every block on the per-direction path
-    constexpr bool kSym = A == 3 && LPR == 1 && !MARLNAV_NO_SYM;
+    constexpr bool kSym = A == 3 && LPR == 1 && !HELP && !MARLNAV_NO_SYM;
     const bool refc = !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f && pr.max_at_prop_d == 2.0f;
     bool sym = false;
     // finished envs re-initialised and re-observed inside the symmetric
@@ -708,6 +875,13 @@ __global__ void __launch_bounds__(64 * A)
                                                          rowv, pr, unused);
         lds_row_write<D>(obs_rows + r * D, rowv);
         if (!OBS_ONLY) red[r] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
+    }
+    if constexpr (HELP) {  // agents 2.. fresh pairs, under the observation phase
+        if (hw && overlap)
+#pragma unroll
+            for (int a = 2; a < A; ++a)
+                helper_fresh_pairs<A, O>(b.formation, a, reinterpret_cast<float(&)[2 * O]>(hfo),
+                                         pr.cap_distance, lds + BP::FR, (int)lane);
     }
     __syncthreads();
     STAMP(3);
@@ -803,6 +977,17 @@ __global__ void __launch_bounds__(64 * A)
                         if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
                     }
                 }
+            }
+        } else if (HELP && overlap) {
+            // ---- the helper wave's finished-env tail (waves 1..A-1 idle)
+            if constexpr (HELP) {
+                if (hw && !(MARLNAV_AB & 1))
+                    helper_tail<A, O, E, D>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM,
+                                            lds + BP::FRESH, lds + BP::FR,
+                                            reinterpret_cast<const float2 *>(K->a.b.formation_obs),
+                                            red, lds + BP::SN,
+                                            reinterpret_cast<const uint8_t *>(lds + BP::TM), ne, pr,
+                                            (int)lane);
             }
         } else if (overlap && !early) {
             // ---- waves 1..A-1, while wave 0 runs the per-env phase: the

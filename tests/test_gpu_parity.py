@@ -194,8 +194,8 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
     chunks): the GPU trajectory equals the oracle's bit for bit. The ragged
     split-kernel cases end on a workgroup with fewer live waves (1021 = 255*4
     + 1 one-env waves) and a partial tile (1003 envs, two per LPR-8 wave).
-    The env-block kernel runs with 4 lanes per agent row at 16384 and 8195
-    envs (ragged last block) and with 2 at 32773 (block_lpr_for)."""
+    At 16384 and 8195 envs (ragged last block) the env-block kernel runs
+    with its helper wave (at most 256 blocks)."""
     g = torch.Generator().manual_seed(P + A + O)
     env = make_env(pkg, P, A, O, episode_len=ep, seed=99,
                    factors=dict(risk_factor=3., distance_factor=7.))
@@ -1004,7 +1004,7 @@ def test_non_finite_env_reinitialised_like_the_reference_blend(pkg, P, A, O):
                    np.zeros(P, np.bool_), acts, form=form, where=f"P{P} A{A} O{O}")
 
 
-@pytest.mark.parametrize("lpr", [1, 2, 4])
+@pytest.mark.parametrize("lpr", [1, 2, 4, "helper"])
 @pytest.mark.parametrize("case", ["native", "non_finite", "reference_rng", "extreme"])
 def test_block_lanes_per_row_bit_exact_vs_oracle(pkg, lpr, case):
     """The env-block kernel at each lanes-per-row setting (1: the symmetric
@@ -1014,8 +1014,13 @@ def test_block_lanes_per_row_bit_exact_vs_oracle(pkg, lpr, case):
     (many finished envs every step), non-finite states / obstacles / targets
     blended like the reference, reference-RNG fresh candidates, and extreme
     coordinates that take the IEEE pair math - every output bit for bit
-    against the oracle."""
+    against the oracle. "helper": one lane per row with the fourth (helper)
+    wave forced on - the fresh draws and the fresh env's obstacle pairs
+    precomputed by it, the finished envs' rows copied from the formation
+    template and its table, or recomputed where an old value is non-finite."""
     P, A, O = 4096 + 5, 3, 3
+    helper = lpr == "helper"
+    lpr = 1 if helper else lpr
     g = torch.Generator().manual_seed(17 + lpr)
     ref = case == "reference_rng"
     env = make_env(pkg, P, A, O, episode_len=3, seed=31, rng="reference" if ref else "native",
@@ -1024,6 +1029,7 @@ def test_block_lanes_per_row_bit_exact_vs_oracle(pkg, lpr, case):
     lib = env._lib
     prev_f = lib.marlnav_debug_force_family(1)
     prev_l = lib.marlnav_debug_force_block_lpr(lpr)
+    prev_h = lib.marlnav_debug_force_helper(1 if helper else 0)
     try:
         st, ob, tg = (env.states.cpu().clone(), env.obstacles.cpu().clone(),
                       env.target.cpu().clone())
@@ -1052,6 +1058,7 @@ def test_block_lanes_per_row_bit_exact_vs_oracle(pkg, lpr, case):
                        where=f"LPR {lpr} {case}")
         assert lib.marlnav_debug_last_family() == 1
     finally:
+        lib.marlnav_debug_force_helper(prev_h)
         lib.marlnav_debug_force_block_lpr(prev_l)
         lib.marlnav_debug_force_family(prev_f)
 
