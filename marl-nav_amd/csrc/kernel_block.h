@@ -800,9 +800,9 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // ---- observations of the moved state + reward terms (:99-100)
     float4 *red = reinterpret_cast<float4 *>(lds + BP::RED);
     float *obs_rows = lds + BP::OBS;
-    // agent-pair symmetry (block_observe_sym): FAST A3 blocks; the A/B
-    // switch MARLNAV_NO_SYM keeps every block on the per-direction path
-    constexpr bool kSym = A == 3 && LPR == 1 && !HELP && !MARLNAV_NO_SYM;
+    // agent-pair symmetry (block_observe_sym): FAST A3 blocks of A/B builds
+    // with MARLNAV_SYM (no faster than the per-direction rows: DESIGN.md §5)
+    constexpr bool kSym = A == 3 && LPR == 1 && !HELP && MARLNAV_SYM;
     const bool refc = !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f && pr.max_at_prop_d == 2.0f;
     bool sym = false;
     // finished envs re-initialised and re-observed inside the symmetric
@@ -813,7 +813,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
         if (__builtin_expect(fast, 1)) {
             float2 *pt = reinterpret_cast<float2 *>(lds + BP::PT);
             const float *obe = lds + BP::OB + 2 * O * l, *tge = lds + BP::TG + 2 * l;
-            if constexpr (!OBS_ONLY && kPre && !(MARLNAV_AB & 1) && !MARLNAV_NO_EARLY) {
+            if constexpr (!OBS_ONLY && kPre && !(MARLNAV_AB & 1) && MARLNAV_EARLY) {
                 early = overlap;
                 if (early) {
                     const EarlyReinit er{kargs_late<kHotKargsOff>(), lds + BP::FORM, lds + BP::FRESH,
