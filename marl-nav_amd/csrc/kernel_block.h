@@ -784,9 +784,11 @@ __global__ void __launch_bounds__(64 * (A + HELP))
             helper_fresh_pairs<A, O>(b.formation, 1, reinterpret_cast<float(&)[2 * O]>(hfo),
                                      pr.cap_distance, lds + BP::FR, (int)lane);
     }
-    if (full && !hw) {
-        crange.add(ox);
-        crange.add(oy);
+    if (full) {
+        if (!hw) {  // (the helper's share of the obstacle / target check still counts)
+            crange.add(ox);
+            crange.add(oy);
+        }
         // one word for the block, written only by waves that found one (all
         // write 1: a benign race); read once after the barrier
         const bool bad = __ballot(!crange.ok()) != 0ull;
@@ -913,6 +915,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
                 float rv[A];
 #pragma unroll
                 for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
+                STAMPX(0);  // (wave 0: the reward terms read)
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
                 if (!(MARLNAV_AB & 1024))  // (AB 1024: timing only, no per-env stores)
                 out_el(b.reward, e, rsum / (float)A);              // torch.mean (:233)
@@ -957,6 +960,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
                 co_l = any_col;
                 ta_l = all_in;
             }
+            STAMPX(1);  // (wave 0: the per-env outputs issued)
             const uint64_t finmask = __ballot(fin);
             if (fin)
                 list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
@@ -978,6 +982,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
                     }
                 }
             }
+            STAMPX(2);  // (wave 0: list, counts and counters done)
         } else if (HELP && overlap) {
             // ---- the helper wave's finished-env tail (waves 1..A-1 idle)
             if constexpr (HELP) {

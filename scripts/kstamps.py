@@ -150,6 +150,19 @@ def main():
                       round(float(np.median(ph[reo][m, 3])), 3), "sub-phases", out,
                       "nfin histogram", {int(k): int(v) for k, v in
                                          zip(*np.unique(raw[reo][m, 19], return_counts=True))})
+        # wave 0's per-env phase (STAMPX 0..2 in wave 0: reward terms read,
+        # outputs issued, list / counters done), every block
+        w0 = (gidx % int(os.environ.get("WPB", str(A)))) == 0
+        if w0.any():
+            x = raw[w0][:, 20:23] * 10.0 / 1e3
+            t3, t4 = rt[w0][:, 3], rt[w0][:, 4]
+            ok = (x > 0).all(axis=1)
+            if ok.any():
+                seq = [("observed", t3), ("terms_read", x[:, 0]), ("outputs_issued", x[:, 1]),
+                       ("counters_done", x[:, 2]), ("env_barrier", t4)]
+                out = {f"{a}->{b}": round(float(np.median((tb - ta)[ok])), 3)
+                       for (a, ta), (b, tb) in zip(seq, seq[1:])}
+                print(cfg, "wave-0 per-env sub-phases (median us):", out)
         del env
 
 
