@@ -210,17 +210,6 @@ int marlnav_debug_force_family(int family);
  * this thread launched. */
 int marlnav_debug_last_family(void);
 
-/* Testing hook: lanes per agent row of the env-block kernel (1, 2 or 4;
- * 0 = automatic, by grid size), process-wide; shapes compiled without that
- * variant take the largest compiled one below it. Returns the previous
- * setting. */
-int marlnav_debug_force_block_lpr(int lpr);
-
-/* Testing hook: the env-block kernel's helper wave (A3/O3 native re-init
- * steps): -1 automatic (grids of at most 256 blocks), 0 never, 1 always.
- * Returns the previous setting. */
-int marlnav_debug_force_helper(int on);
-
 /* Testing hook (not part of the reference's interface): the step kernels'
  * bearing acos (environment.py:286) of the n consecutive fp32 bit patterns
  * from `first`, into the device array out[n] (tests/golden/acos_dev_check.py

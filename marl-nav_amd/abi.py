@@ -65,8 +65,7 @@ EXPORTS = ("marlnav_step", "marlnav_observe", "marlnav_reinit_all", "marlnav_for
            "marlnav_returns_work_size", "marlnav_discounted_returns",
            "marlnav_last_error", "marlnav_abi_version",
            "marlnav_debug_force_family", "marlnav_debug_last_family",
-           "marlnav_debug_acos_range", "marlnav_debug_force_block_lpr",
-           "marlnav_debug_force_helper")
+           "marlnav_debug_acos_range")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmarlnav.so")
@@ -102,12 +101,6 @@ def _declare(lib):
     lib.marlnav_debug_force_family.restype = c.c_int
     lib.marlnav_debug_last_family.argtypes = []
     lib.marlnav_debug_last_family.restype = c.c_int
-    if hasattr(lib, "marlnav_debug_force_helper"):  # (absent from older A/B builds)
-        lib.marlnav_debug_force_helper.argtypes = [c.c_int]
-        lib.marlnav_debug_force_helper.restype = c.c_int
-    if hasattr(lib, "marlnav_debug_force_block_lpr"):  # (absent from older A/B builds)
-        lib.marlnav_debug_force_block_lpr.argtypes = [c.c_int]
-        lib.marlnav_debug_force_block_lpr.restype = c.c_int
     if hasattr(lib, "marlnav_debug_acos_range"):  # (absent from A/B builds of older revisions)
         lib.marlnav_debug_acos_range.argtypes = [c.c_uint32, c.c_int64, c.c_void_p, c.c_void_p]
         lib.marlnav_debug_acos_range.restype = c.c_int

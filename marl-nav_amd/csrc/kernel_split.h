@@ -747,9 +747,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             stamp_nfin = list.total();
 #endif
             if (const int nfin = (MARLNAV_AB & 1) ? 0 : list.total()) {  // (AB 1: timing only)
-                // (A/B: the workgroups that carry the launch's tail first in
-                // every SIMD's issue arbitration)
-                if (MARLNAV_TAIL_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_TAIL_PRIO);
                 KArgsK *kl = kargs_late<kHotKargsOff>();
                 const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
                     lds, blk0 * EPW};

@@ -50,19 +50,3 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_AB_NOREFC
 #define MARLNAV_AB_NOREFC 0
 #endif
-// A/B variant: the env-block kernel with agent-pair symmetry at A3
-// (block_observe_sym; measured no faster than the per-direction rows,
-// DESIGN.md §5, so off in the product build)
-#ifndef MARLNAV_SYM
-#define MARLNAV_SYM 0
-#endif
-// A/B variant (with MARLNAV_SYM): finished envs re-initialised inside the
-// symmetric observation phase (measured slower)
-#ifndef MARLNAV_EARLY
-#define MARLNAV_EARLY 0
-#endif
-// A/B variant: s_setprio level of the waves that re-initialise finished envs
-// (the launch's tail), 0 = none
-#ifndef MARLNAV_TAIL_PRIO
-#define MARLNAV_TAIL_PRIO 0
-#endif

@@ -310,64 +310,30 @@ int launch_split(const SplitVariant &v, BlockFn fn, const StepArgs &args, const 
     return 0;
 }
 
-// env-block kernels (block_kernel) for these shapes, at LPR lanes per agent
-// row (E = 64 / LPR envs per block)
+// env-block kernels (block_kernel) for these shapes
 struct BlockVariant {
-    int A, O, lpr;
+    int A, O;
     BlockFn step, obs, noisy;
     size_t lds;
 };
 
-#define MARLNAV_BLOCK_VARIANT(A, O, LPR)                                               \
-    {A, O, LPR, block_kernel<A, O, false, false, LPR>, block_kernel<A, O, true, false, LPR>, \
-     block_kernel<A, O, false, true, LPR>, (size_t)BlockPlan<A, O, LPR>::FLOATS * 4}
+#define MARLNAV_BLOCK_VARIANT(A, O)                                                    \
+    {A, O, block_kernel<A, O, false, false>, block_kernel<A, O, true, false>,          \
+     block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4}
 const BlockVariant kBlockVariants[] = {
-    MARLNAV_BLOCK_VARIANT(3, 3, 1),
-    MARLNAV_BLOCK_VARIANT(3, 3, 2),
-    MARLNAV_BLOCK_VARIANT(3, 3, 4),
-    MARLNAV_BLOCK_VARIANT(3, 8, 1),
-    MARLNAV_BLOCK_VARIANT(3, 1, 1),
-    MARLNAV_BLOCK_VARIANT(2, 1, 1),
+    MARLNAV_BLOCK_VARIANT(3, 3),
+    MARLNAV_BLOCK_VARIANT(3, 8),
+    MARLNAV_BLOCK_VARIANT(3, 1),
+    MARLNAV_BLOCK_VARIANT(2, 1),
 };
 #undef MARLNAV_BLOCK_VARIANT
-
-// Lanes per agent row. Automatic: 1. The 2- and 4-lane forms give small
-// grids three waves per SIMD but repeat each row's stage / move / per-env
-// instruction stream on every lane group's wave, and measured slower than
-// one lane per row (graph replay, same box: 16384x3x3 5.34 us at LPR 1 against
-// 5.54 at 2 and 5.75 at 4; 32768x3x3 6.26 / 6.25 / -); they are
-// kept for marlnav_debug_force_block_lpr and the A/B builds
-// (MARLNAV_BLOCK_LPR).
-#ifndef MARLNAV_BLOCK_LPR
-#define MARLNAV_BLOCK_LPR 0
-#endif
-#ifndef MARLNAV_BLOCK_LPR_AUTO
-#define MARLNAV_BLOCK_LPR_AUTO 0
-#endif
-constexpr int64_t kBlockWavesTarget = 3072;
-std::atomic<int> g_block_lpr{0};  // marlnav_debug_force_block_lpr (0: automatic)
-
-int block_lpr_for(int64_t P, int A)
-{
-    if (MARLNAV_BLOCK_LPR) return MARLNAV_BLOCK_LPR;
-    if (const int f = g_block_lpr.load(std::memory_order_relaxed)) return f;
-    if (MARLNAV_BLOCK_LPR_AUTO) {  // (the grid-filling rule, A/B builds)
-        int lpr = 1;
-        while (lpr < 4 && (P + 64 / lpr - 1) / (64 / lpr) * A < kBlockWavesTarget) lpr *= 2;
-        return lpr;
-    }
-    return 1;
-}
 
 const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers &b, bool obs_only)
 {
     if (d->obstacle_stride != d->num_obstacles) return nullptr;
     const BlockVariant *v = nullptr;
-    const int want = block_lpr_for(d->num_parallel, d->num_agents);
-    for (const BlockVariant &x : kBlockVariants)  // the wanted LPR, else the largest compiled below it
-        if (x.A == d->num_agents && x.O == d->num_obstacles && x.lpr <= want &&
-            (!v || x.lpr > v->lpr))
-            v = &x;
+    for (const BlockVariant &x : kBlockVariants)
+        if (x.A == d->num_agents && x.O == d->num_obstacles) v = &x;
     if (!v) return nullptr;
     if (!aligned(b.states, 16) || !aligned(b.obstacles, 16) || !aligned(b.target, 16) ||
         !aligned(b.obs, 16) || (b.states_out && !aligned(b.states_out, 16)))
@@ -378,31 +344,13 @@ const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers 
     return v;
 }
 
-// The env-block kernel with a helper wave (kernel_block.h, HELP) for grids
-// of at most kHelpMaxBlocksPerCu blocks per CU: the native (non-noisy) re-init
-// step of the A3/O3 shape, with the formation template.
-constexpr int64_t kHelpMaxBlocks = 256;  // one 4-wave block per CU
-#ifndef MARLNAV_NO_HELP
-#define MARLNAV_NO_HELP 0
-#endif
-std::atomic<int> g_help{-1};  // marlnav_debug_force_helper: -1 automatic, 0 off, 1 on
-
-bool use_helper(const MarlnavDims *d, const MarlnavStepBuffers &b, bool noisy)
-{
-    if (MARLNAV_NO_HELP || noisy || b.fresh_states || !b.formation || !b.formation_obs) return false;
-    if (d->num_agents != 3 || d->num_obstacles != 3 || d->obstacle_stride != 3) return false;
-    const int f = g_help.load(std::memory_order_relaxed);
-    if (f >= 0) return f == 1;
-    return (d->num_parallel + 63) / 64 <= kHelpMaxBlocks;
-}
-
 int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const MarlnavParams &pr,
-                 void *stream, const char *what, bool help = false)
+                 void *stream, const char *what)
 {
     KArgs ka;
     ka.a = args;
     ka.p = pr;
-    ka.a.W = 64 / v.lpr;  // envs per block
+    ka.a.W = BlockPlan<3, 3>::E;
     ka.a.ntiles = (args.P + ka.a.W - 1) / ka.a.W;
     // the leading arguments (kHotKargsOff, kernel_args.h): staging pointers, P
     float *h_states = args.b.states;
@@ -412,10 +360,8 @@ int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const 
     int64_t h_P = args.P;
     void *kargs[] = {&h_states, &h_actions, &h_obstacles, &h_target, &h_step_num, &h_terminates,
                      &h_P, &ka};
-    const size_t lds = help ? (size_t)BlockPlan<3, 3, 1, true>::FLOATS * 4 : v.lds;
     hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)ka.a.ntiles),
-                                   dim3(64 * (v.A + (help ? 1 : 0))), kargs, lds,
-                                   (hipStream_t)stream);
+                                   dim3(64 * v.A), kargs, v.lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
     return 0;
@@ -491,19 +437,6 @@ int marlnav_debug_force_family(int family)
 }
 
 int marlnav_debug_last_family(void) { return g_last_family; }
-
-int marlnav_debug_force_helper(int on)
-{
-    if (on < -1 || on > 1) return fail(MARLNAV_EINVAL, "helper wave %d: -1 (automatic), 0 or 1", on);
-    return g_help.exchange(on, std::memory_order_relaxed);
-}
-
-int marlnav_debug_force_block_lpr(int lpr)
-{
-    if (lpr != 0 && lpr != 1 && lpr != 2 && lpr != 4)
-        return fail(MARLNAV_EINVAL, "lanes per row %d: 0 (automatic), 1, 2 or 4", lpr);
-    return g_block_lpr.exchange(lpr, std::memory_order_relaxed);
-}
 
 #if MARLNAV_STAMPS
 int marlnav_debug_stamps(void *buf)
@@ -600,9 +533,6 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
     if (family_allowed(MARLNAV_FAMILY_BLOCK))
         if (const BlockVariant *v = select_block(d, args.b, false)) {
             g_last_family = MARLNAV_FAMILY_BLOCK;
-            if (v->lpr == 1 && use_helper(d, args.b, noisy))
-                return launch_block(*v, block_kernel<3, 3, false, false, 1, true>, args, *pr, stream,
-                                    "marlnav_step", true);
             return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }
     const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);

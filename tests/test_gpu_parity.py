@@ -194,8 +194,8 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
     chunks): the GPU trajectory equals the oracle's bit for bit. The ragged
     split-kernel cases end on a workgroup with fewer live waves (1021 = 255*4
     + 1 one-env waves) and a partial tile (1003 envs, two per LPR-8 wave).
-    At 16384 and 8195 envs (ragged last block) the env-block kernel runs
-    with its helper wave (at most 256 blocks)."""
+    16384 (configs[4]'s per-GPU shape), 8195 (ragged last block) and 32773
+    envs at 3-step and shorter episodes: many finished envs every step."""
     g = torch.Generator().manual_seed(P + A + O)
     env = make_env(pkg, P, A, O, episode_len=ep, seed=99,
                    factors=dict(risk_factor=3., distance_factor=7.))
@@ -1002,65 +1002,6 @@ def test_non_finite_env_reinitialised_like_the_reference_blend(pkg, P, A, O):
     acts = [((torch.rand(P, A, 2, generator=g) - 0.5) * 0.8).numpy() for _ in range(4)]
     _run_vs_oracle(env, dm, pr, st.numpy(), ob.numpy(), tg.numpy(), np.zeros(P, np.float32),
                    np.zeros(P, np.bool_), acts, form=form, where=f"P{P} A{A} O{O}")
-
-
-@pytest.mark.parametrize("lpr", [1, 2, 4, "helper"])
-@pytest.mark.parametrize("case", ["native", "non_finite", "reference_rng", "extreme"])
-def test_block_lanes_per_row_bit_exact_vs_oracle(pkg, lpr, case):
-    """The env-block kernel at each lanes-per-row setting (1: the symmetric
-    A3 observation with the finished envs re-initialised inside it; 2 and
-    4: each row's pairs split over neighbouring lanes), forced on the same
-    4101-env grid (a ragged last block): native re-init with 3-step episodes
-    (many finished envs every step), non-finite states / obstacles / targets
-    blended like the reference, reference-RNG fresh candidates, and extreme
-    coordinates that take the IEEE pair math - every output bit for bit
-    against the oracle. "helper": one lane per row with the fourth (helper)
-    wave forced on - the fresh draws and the fresh env's obstacle pairs
-    precomputed by it, the finished envs' rows copied from the formation
-    template and its table, or recomputed where an old value is non-finite."""
-    P, A, O = 4096 + 5, 3, 3
-    helper = lpr == "helper"
-    lpr = 1 if helper else lpr
-    g = torch.Generator().manual_seed(17 + lpr)
-    ref = case == "reference_rng"
-    env = make_env(pkg, P, A, O, episode_len=3, seed=31, rng="reference" if ref else "native",
-                   factors=dict(risk_factor=3., distance_factor=7., bond_factor=2.),
-                   **({"noise_device": "cpu"} if ref else {}))
-    lib = env._lib
-    prev_f = lib.marlnav_debug_force_family(1)
-    prev_l = lib.marlnav_debug_force_block_lpr(lpr)
-    prev_h = lib.marlnav_debug_force_helper(1 if helper else 0)
-    try:
-        st, ob, tg = (env.states.cpu().clone(), env.obstacles.cpu().clone(),
-                      env.target.cpu().clone())
-        if case == "non_finite":
-            st[3, 0, 0] = float("nan")
-            st[70, 1, 2:4] = torch.tensor([float("inf"), 0.0])
-            ob[140, 0, 1] = float("nan")
-            tg[255, 0, 0] = float("inf")
-        if case == "extreme":
-            st[100:140, :, 0] *= 3e12   # far beyond the fast coordinate range
-            ob[300:310] *= 1e-30
-        env.states, env.obstacles, env.target = st, ob, tg
-        dm, pr = oracle_params(env)
-        form = np_(env._formation)
-        acts = [((torch.rand(P, A, 2, generator=g) - 0.5) * 0.8).numpy() for _ in range(5)]
-        fresh = None
-        if case == "reference_rng":
-            fresh = []
-            for _ in acts:
-                fs = np.random.default_rng(len(fresh)).uniform(-60, 60, (P, A, 5)).astype(np.float32)
-                fo = np.random.default_rng(len(fresh) + 9).uniform(-300, 300, (P, O, 2)).astype(np.float32)
-                ft = np.random.default_rng(len(fresh) + 99).uniform(-300, 300, (P, 1, 2)).astype(np.float32)
-                fresh.append((fs, fo, ft))
-        _run_vs_oracle(env, dm, pr, st.numpy(), ob.numpy(), tg.numpy(), np.zeros(P, np.float32),
-                       np.zeros(P, np.bool_), acts, form=form, fresh_list=fresh,
-                       where=f"LPR {lpr} {case}")
-        assert lib.marlnav_debug_last_family() == 1
-    finally:
-        lib.marlnav_debug_force_helper(prev_h)
-        lib.marlnav_debug_force_block_lpr(prev_l)
-        lib.marlnav_debug_force_family(prev_f)
 
 
 @pytest.mark.parametrize("P,A,O", [(20000 + 13, 3, 3), (300, 3, 3), (60, 3, 3), (512, 16, 32)])
