@@ -311,22 +311,21 @@ __device__ __forceinline__ void div2_fast(float x, float y, float den, float *qx
 }
 
 // acos of the bearing (environment.py:286): the device library's acosf
-// sequence (ROCm ocml, as hipcc compiles it for gfx950: r = |x| > 0.5 ?
-// 0.5 - 0.5|x| : x*x, u = r * P5(r); |x| <= 0.5: pi/2 - (x + x*u);
-// |x| > 0.5: 2(s + s*u), or pi minus that for x < 0, s = sqrt(r)) written out
-// here with one change: s is the correctly rounded sqrt (sqrt_fast, exact on
-// r = 0 and on every r >= 2^-96) where the library uses v_sqrt_f32, which
-// differs from it on 9% of the r this sequence feeds it (1 520 276 of the
-// 2 130 706 434 fp32 inputs in [-1, 1] change: tests/golden/MANIFEST.json
-// "acos_device"). With every step an IEEE operation, oracle/marlnav_oracle.c
-// acos_device restates it bit for bit, so the bearings are compared with the
-// oracle exactly. MARLNAV_LIB_ACOS builds the library's acosf instead (A/B).
-#ifndef MARLNAV_LIB_ACOS
-#define MARLNAV_LIB_ACOS 0
+// (ROCm ocml: a degree-5 polynomial in r = |x| > 0.5 ? 0.5 - 0.5|x| : x*x,
+// with a v_sqrt_f32 of r on the |x| > 0.5 branch). oracle/marlnav_oracle.c
+// acos_device restates it op for op; the hardware sqrt, which is not
+// correctly rounded, is restated from an exhaustive measurement of it on the
+// only r that branch produces (k * 2^-25, tests/golden/vsqrt_r_grid.npz), so
+// kernel and oracle bearings agree bit for bit (tests/golden/acos_dev_check.py
+// checks every fp32 in [-1, 1]). MARLNAV_ACOS_CR_SQRT (A/B builds): the same
+// sequence with the correctly rounded sqrt (sqrt_fast) - five more VALU per
+// bearing, measured +0.24 us at 16384x3x3 and +0.32 us at 4096x16x32.
+#ifndef MARLNAV_ACOS_CR_SQRT
+#define MARLNAV_ACOS_CR_SQRT 0
 #endif
 __device__ __forceinline__ float acos_k(float x)
 {
-    if (MARLNAV_LIB_ACOS) return acosf(x);
+    if (!MARLNAV_ACOS_CR_SQRT) return acosf(x);
     const float ax = fabsf(x);
     const float rt = __builtin_fmaf(ax, -0.5f, 0.5f);
     const float x2 = x * x;

@@ -16,6 +16,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "liboracle.so")
+VSQRT_GRID = os.path.join(os.path.dirname(HERE), "tests", "golden", "vsqrt_r_grid.npz")
 _abi = importlib.import_module("marl-nav_amd.abi")
 _lib = None
 
@@ -62,6 +63,15 @@ def load():
         lib.oracle_acos_device_range.restype = None
         lib.oracle_set_acos_mode.argtypes = [ctypes.c_int]
         lib.oracle_set_acos_mode.restype = None
+        lib.oracle_set_vsqrt_grid.argtypes = [P, ctypes.c_int64, P, ctypes.c_int64]
+        lib.oracle_set_vsqrt_grid.restype = None
+        # the measured v_sqrt_f32 offsets the kernels' acos sees
+        # (tests/golden/vsqrt_r_grid.npz, scripts/probes/vsqrt_grid.py): kept
+        # alive here for the library's lifetime
+        g = np.load(VSQRT_GRID)
+        tab = (np.ascontiguousarray(g["down"], np.uint8), np.ascontiguousarray(g["up"], np.uint32))
+        lib.oracle_set_vsqrt_grid(tab[0].ctypes.data, int(g["n"]), tab[1].ctypes.data, tab[1].size)
+        lib._vsqrt_grid = tab
         lib.oracle_discounted_returns.argtypes = [ctypes.c_int64, ctypes.c_int64, P, P,
                                                   ctypes.c_double, P, P]
         lib.oracle_discounted_returns.restype = None
@@ -208,8 +218,8 @@ def sincos_range(first_bits, n, which=0):
 
 
 def acos_device(x):
-    """The HIP kernel's acos (the device library's acosf, restated) over an
-    array."""
+    """The HIP kernel's acos (the device library's acosf, restated; its
+    hardware sqrt from tests/golden/vsqrt_r_grid.npz) over an array."""
     x = np.ascontiguousarray(x, np.float32).ravel()
     out = np.empty_like(x)
     load().oracle_acos_device_n(x.size, _ptr(x), _ptr(out))

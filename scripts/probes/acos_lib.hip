@@ -18,3 +18,20 @@ extern "C" int acos_dev_range(uint32_t first, int64_t n, void *out, void *stream
                        n, (float *)out);
     return (int)hipGetLastError();
 }
+
+// v_sqrt_f32 (the instruction inside the library's acosf) of r = k * 2^-25
+// for k in [k0, k0 + n): every r the acosf's |x| > 0.5 branch can feed it
+// (r = 0.5 - 0.5|x| with |x| in (0.5, 1] a multiple of 2^-24)
+__global__ void vsqrt_grid_kernel(uint32_t k0, int64_t n, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = __builtin_amdgcn_sqrtf((float)(k0 + (uint32_t)i) * 0x1.0p-25f);
+}
+
+extern "C" int vsqrt_grid(uint32_t k0, int64_t n, void *out, void *stream)
+{
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(vsqrt_grid_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, k0, n,
+                       (float *)out);
+    return (int)hipGetLastError();
+}

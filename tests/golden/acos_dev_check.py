@@ -1,13 +1,14 @@
 """The HIP kernel's acos over every fp32 in [-1, 1] (GPU box; generating script
 for tests/golden/MANIFEST.json "acos_device").
 
-The step kernels evaluate the bearing's acos (environment.py:286) with
-acos_k (marl-nav_amd/csrc/device_math.h): the device library's acosf sequence
-with the correctly rounded sqrt in place of its v_sqrt_f32.
-oracle/marlnav_oracle.c restates it op for op (acos_device). This script runs
-the kernels' acos (libmarlnav.so marlnav_debug_acos_range) and the library's
-own acosf (scripts/probes/acos_lib.hip, built with the product's flags) over
-all 2 130 706 434 inputs in [-1, 1] and compares:
+The step kernels evaluate the bearing's acos (environment.py:286) with the
+device library's acosf (acos_k, marl-nav_amd/csrc/device_math.h).
+oracle/marlnav_oracle.c restates it op for op (acos_device), taking the
+v_sqrt_f32 inside it from the measured table tests/golden/vsqrt_r_grid.npz
+(scripts/probes/vsqrt_grid.py). This script runs the kernels' acos
+(libmarlnav.so marlnav_debug_acos_range) and the library's acosf compiled
+alone (scripts/probes/acos_lib.hip, the product's flags) over all
+2 130 706 434 inputs in [-1, 1] and compares:
 
 * kernel vs the oracle's restatement (must be equal on every input: this is
   what lets the GPU tests compare kernel and oracle bearings bit for bit);
@@ -112,9 +113,10 @@ def main():
             ex += e
     n = int(tot[0])
     res = {
-        "what": "the step kernels' bearing acos (acos_k: the device library's acosf "
-                "sequence with the correctly rounded sqrt) and the library's own acosf "
-                "over every fp32 in [-1, 1], tests/golden/acos_dev_check.py on an MI355X",
+        "what": "the step kernels' bearing acos (acos_k: the device library's acosf) and "
+                "that acosf compiled alone, over every fp32 in [-1, 1], against the oracle's "
+                "restatement (acos_device with the measured v_sqrt_f32 table) and MKL; "
+                "tests/golden/acos_dev_check.py on an MI355X",
         "inputs": n,
         "kernel_equals_oracle_acos_device": int(tot[1]),
         "kernel_not_equal_examples": ex[:8],
