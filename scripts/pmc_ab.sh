@@ -13,6 +13,8 @@ PASSES=(
  "FETCH_SIZE GRBM_GUI_ACTIVE"
  "WRITE_SIZE GRBM_GUI_ACTIVE"
  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_LDS SQ_IFETCH"
+ "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ SQC_ICACHE_MISSES_DUPLICATE SQC_TC_INST_REQ SQ_IFETCH SQ_WAVES SQ_WAVE_CYCLES"
+ "InstrFetchLatency SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES"
 )
 ONLY=${ONLY:-14}
 for lib in ${LIBS:-marl-nav_amd/lib/libmarlnav.so}; do
@@ -35,5 +37,10 @@ g = lambda k: d.get(k, float("nan"))
 print(f"{sys.argv[2]:>14} us {g('kernel_us_median_under_pmc'):.2f} conflict/idx {g('SQ_LDS_BANK_CONFLICT') / g('SQ_LDS_IDX_ACTIVE'):.4f} "
       f"wait/wave {g('SQ_WAIT_ANY') / max(g('SQ_WAVE_CYCLES'), 1):.3f} valu/wave {g('SQ_INSTS_VALU') / max(g('SQ_WAVES'), 1):.0f} "
       f"lds/wave {g('SQ_INSTS_LDS') / max(g('SQ_WAVES'), 1):.0f} waitlds {g('SQ_WAIT_INST_LDS'):.4g}")
+if 'InstrFetchLatency' in d:
+    print(f"{'':>14} ifetch latency {g('InstrFetchLatency'):.0f} cyc  wait_inst/wave {g('SQ_WAIT_INST_ANY') / max(g('SQ_WAVE_CYCLES'), 1):.3f} wait/wave {g('SQ_WAIT_ANY') / max(g('SQ_WAVE_CYCLES'), 1):.3f} wave_cycles/wave {g('SQ_WAVE_CYCLES') / max(g('SQ_WAVES'), 1):.0f}")
+if 'SQC_ICACHE_MISSES' in d:
+    print(f"{'':>14} icache req {g('SQC_ICACHE_REQ'):.0f} miss {g('SQC_ICACHE_MISSES'):.0f} dup {g('SQC_ICACHE_MISSES_DUPLICATE'):.0f} "
+          f"tc_inst {g('SQC_TC_INST_REQ'):.0f} ifetch/wave {g('SQ_IFETCH') / max(g('SQ_WAVES'), 1):.1f}")
 PY
 done
