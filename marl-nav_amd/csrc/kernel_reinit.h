@@ -508,6 +508,18 @@ __device__ __forceinline__ void reinit_reobs_tpl(KArgsK *kl, const Envs &ev, con
     }
 }
 
+// A wave-uniform ballot mask as a list: entry fe is the env code of the
+// fe-th set bit (scalar bit clears; fe is wave-uniform)
+struct BitList {
+    uint64_t fm;
+    __device__ int operator[](int fe) const
+    {
+        uint64_t m = fm;
+        for (int i = 0; i < fe; ++i) m &= m - 1ull;
+        return (int)__builtin_ctzll(m);
+    }
+};
+
 // The finished envs of a block as a wave-uniform ballot mask (env code = bit
 // position; the env-block kernel): entry fe is the fe-th set bit, found by
 // scalar bit scans over the few entries one pass of items touches - no LDS

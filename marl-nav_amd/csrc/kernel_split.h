@@ -106,6 +106,14 @@ constexpr bool kSplitRRLeader = !kSplitSpread<A, O> || O <= 8 || MARLNAV_SPLIT_R
 template <int A, int O>
 constexpr bool kSplitTplPass = kSplitTpl<A, O> && (64 * kWavesPerBlock) % O == 0;
 
+// ... and that pass run by waves 1..3 while wave 0 finishes the rows' rewards
+// and the per-env phase (the A3 env-block kernel's overlap): each wave parks
+// its envs' collision bits with their step numbers and `terminates` flags, so
+// the other waves find the finished set without waiting for wave 0
+template <int A, int O>
+constexpr bool kSplitOverlap = kSplitTplPass<A, O> && !kSplitRRLeader<A, O> &&
+                               (64 * (kWavesPerBlock - 1)) % O == 0 && MARLNAV_SPLIT_OVERLAP;
+
 // Extra LDS cycles of the workgroup-spread row-reward read (kernel_split.h,
 // wave 0, lane = tile cw * R + row rw, reading the row's K bond terms at
 // tile base cw * F + BOND, row stride K, one ds_read_b32 per term): banks are
@@ -177,10 +185,11 @@ struct SplitPlan {
     // after the waves' regions: finished-env counts and slots of the
     // workgroup, the `unclean` word (reinit_block), then (kSplitTpl) the
     // formation and template at FTP
-    // (+ kWavesPerBlock * EPW step numbers and as many `terminates` flags:
-    // the workgroup's per-env inputs, parked for wave 0's per-env phase)
+    // (+ kWavesPerBlock * EPW step numbers and as many `terminates` flags and
+    // collision bits: the workgroup's per-env inputs, parked for wave 0's
+    // per-env phase and (kSplitOverlap) the other waves' finished set)
     static constexpr int ENVIN = (kWavesPerBlock * (1 + EPW) + 1 + 3) & ~3;
-    static constexpr int FTP = (ENVIN + 2 * kWavesPerBlock * EPW + 3) & ~3;
+    static constexpr int FTP = (ENVIN + 3 * kWavesPerBlock * EPW + 3) & ~3;
     // then (kSplitSpread shapes with O <= 8, native re-init) the fresh
     // obstacle draws of the workgroup's EW envs, component k of obstacle j of
     // env code c at PRE + (2j + k) * EW + c (kernel_reinit.h native_obst_draws)
@@ -557,6 +566,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     const float *tge = wl + SP::TG + 2 * el;
     float *orow = wl + SP::OBS + rowc * SP::DP;
     float *brow = wl + SP::BOND + rowc * (A - 1);
+    uint64_t colm = 0ull;  // row leaders of rows that collided (kSplitOverlap)
     {
         // wave-uniform choice of the pair math (coord_ok);
         // worth its check only when each lane evaluates many pairs
@@ -584,6 +594,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         if (!OBS_ONLY) {
             const unsigned fl = lpr_or<LPR>(t.fl);
             const int band = lpr_sum<LPR>(t.band);
+            if constexpr (kSplitOverlap<A, O>) colm = __ballot(row_on && q == 0 && (fl & 10u));
             wave_sync();  // bond terms of the row are in LDS
             if (row_on && q == 0) {
                 if constexpr (kSplitTgtInAg<A, O, LPR> || kSplitTgtInOb<A, O, LPR>) {
@@ -689,6 +700,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             int *unclean = bslot + kWavesPerBlock * EPW;
             float *bsn = reinterpret_cast<float *>(bcnt) + SP::ENVIN;
             unsigned *bterm = reinterpret_cast<unsigned *>(bsn + kWavesPerBlock * EPW);
+            unsigned *bcol = bterm + kWavesPerBlock * EPW;
+            // waves 1..3 re-initialise under wave 0's per-env phase
+            const bool ovl = kSplitOverlap<A, O> && !NOISY && tpl_on && live == kWavesPerBlock;
             if (threadIdx.x == 0) *unclean = 0;
             if (tpl_on) {  // (uniform: every wave holds its part)
                 float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
@@ -701,6 +715,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             if (env_on) {
                 bsn[wib * EPW + (int)lane] = sn_in;
                 bterm[wib * EPW + (int)lane] = term_in;
+                if constexpr (kSplitOverlap<A, O>) {
+                    // this env's rows: lanes [lane, lane + 1) * A * LPR
+                    constexpr int LE = A * LPR;
+                    const uint64_t emask = LE == 64 ? ~0ull : ((1ull << (LE % 64)) - 1ull);
+                    bcol[wib * EPW + (int)lane] = ((colm >> (((int)lane * LE) % 64)) & emask) != 0ull;
+                }
             }
             __syncthreads();
             STAMP(4);
@@ -739,6 +759,27 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 c_col = __popcll(__ballot(co_l));
                 c_tar = __popcll(__ballot(ta_l));
                 STAMPX(1);
+            } else if constexpr (kSplitOverlap<A, O>) {
+                if (ovl) {
+                    // the finished set from the parked inputs (the same tests
+                    // as per_env: :96-97, :102-104, :213-214), then the
+                    // one-pass re-init and re-observation on 64 * 3 threads
+                    const int ce = (int)lane;
+                    const bool on = ce < live * EPW && blk0 * EPW + ce < P;
+                    const bool fin = on && (bsn[ce] + 1.0f > pr.trunc_after || bterm[ce] != 0u ||
+                                            bcol[ce] != 0u);
+                    const uint64_t fm = __ballot(fin);
+                    if (fm && !(MARLNAV_AB & 1)) {  // (AB 1: timing only)
+                        KArgsK *kl = kargs_late<kHotKargsOff>();
+                        const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP>
+                            ev{lds, blk0 * EPW};
+                        const float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
+                        reinit_reobs_tpl<A, O, 64 * (kWavesPerBlock - 1)>(
+                            kl, ev, ftp, reinterpret_cast<const float2 *>(ftp + SP::NF),
+                            BitList{fm}, (int)__popcll(fm), pr.cap_distance,
+                            (int)threadIdx.x - 64, unclean);
+                    }
+                }
             }
             __syncthreads();
             STAMPX(2);
@@ -754,7 +795,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 const int tid = (int)threadIdx.x, nt = 64 * live;
                 // fused native re-init + re-observation recomputes a Philox
                 // block per obstacle pair: only for few obstacles
-                if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
+                if (ovl) {  // the pass ran above
+                    if (*unclean) {  // an agent or target off the formation: every pair
+                        reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
+                        __syncthreads();
+                    }
+                } else if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
                     reinit_reobs_native<A, O, SP::EW>(kl, ev, kl->a.b.formation, list, nfin,
                                                       pr.cap_distance, tid, nt, pre);
                     __syncthreads();
@@ -840,7 +886,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             if (VAL % 16 == 0) {
                 for (int i = (int)lane; i < n / 4; i += 64) {
                     const int rr = i / D4, c4 = i - rr * D4;
-                    const float4 v = *reinterpret_cast<const float4 *>(src + rr * SP::DP + 4 * c4);
+                    // (AB 2048: timing only - consecutive pieces, no bank
+                    // conflicts: the most an XOR swizzle of the pieces can save)
+                    const float4 v = *reinterpret_cast<const float4 *>(
+                        (MARLNAV_AB & 2048) ? src + 4 * i : src + rr * SP::DP + 4 * c4);
                     if (kWtOut && wt)
                         wt_st4(out_buf(gobs, 4u * n), 16u * i, v);
                     else

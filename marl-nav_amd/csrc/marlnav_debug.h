@@ -50,3 +50,12 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_AB_NOREFC
 #define MARLNAV_AB_NOREFC 0
 #endif
+// Split kernel, workgroup-spread many-obstacle shapes: the one-pass re-init
+// on waves 1..3 under wave 0's per-env phase (1, A/B builds) or after it (0).
+// Measured slower at 4096x16x32 (graph replay 11.81 -> 12.31 us, rocprof
+// 12.74 -> 13.40 us over 200 steps from a fresh env) although the stamps
+// build shows the workgroups with finished envs 0.7 us shorter: their tail
+// then competes with the other workgroups' observe phase for the SIMDs.
+#ifndef MARLNAV_SPLIT_OVERLAP
+#define MARLNAV_SPLIT_OVERLAP 0
+#endif
