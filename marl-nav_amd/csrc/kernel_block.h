@@ -378,6 +378,7 @@ __global__ void __launch_bounds__(64 * A)
         const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
         // ---- per-env reductions, terminal logic (wave 0, one lane per env)
         if (w == 0) {
+            if (MARLNAV_ENV_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_ENV_PRIO);  // (A/B builds)
             const bool env_on = l < ne;
             bool fin = false, tr_l = false, co_l = false, ta_l = false;
             if (env_on) {
@@ -463,6 +464,7 @@ __global__ void __launch_bounds__(64 * A)
                 }
             }
             STAMPX(2);  // (wave 0: list, counts and counters done)
+            if (MARLNAV_ENV_PRIO) __builtin_amdgcn_s_setprio(0);
         } else if (overlap) {
             // ---- waves 1..A-1, while wave 0 runs the per-env phase: the
             // finished set from the inputs wave 0 uses (red flags, step_num,

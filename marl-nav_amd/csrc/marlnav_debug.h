@@ -59,3 +59,7 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_SPLIT_OVERLAP
 #define MARLNAV_SPLIT_OVERLAP 0
 #endif
+// Env-block kernel: wave 0's per-env phase at this s_setprio (A/B builds)
+#ifndef MARLNAV_ENV_PRIO
+#define MARLNAV_ENV_PRIO 0
+#endif
