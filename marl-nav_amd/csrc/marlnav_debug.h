@@ -59,7 +59,11 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_SPLIT_OVERLAP
 #define MARLNAV_SPLIT_OVERLAP 0
 #endif
-// Env-block kernel: wave 0's per-env phase at this s_setprio (A/B builds)
+// Env-block kernel: wave 0's per-env phase (the block's latency chain while
+// its other waves wait at the barrier) at this s_setprio over the other
+// blocks' waves on its SIMD. A/B (profiles/r04_ab_env_prio.txt, graph
+// replay, steady / fresh): 0 -> 3: 65536x3x3 7.00 -> 6.95 / 7.24 -> 7.16 us,
+// 16384x3x3 5.34 -> 5.30 / 5.36 -> 5.34 us.
 #ifndef MARLNAV_ENV_PRIO
-#define MARLNAV_ENV_PRIO 0
+#define MARLNAV_ENV_PRIO 3
 #endif
