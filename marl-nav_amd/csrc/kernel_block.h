@@ -482,6 +482,7 @@ __global__ void __launch_bounds__(64 * A)
             const uint64_t fm = __ballot(fin);
             STAMPX(0);
             if (fm && !(MARLNAV_AB & 1)) {
+                if (MARLNAV_TAIL_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_TAIL_PRIO);  // (A/B builds)
                 STAMPX(1);
                 reinit_reobs_native<A, O, kPre ? E : 0>(kargs_late<kHotKargsOff>(), ev,
                                                         lds + BP::FORM, MaskList{fm},

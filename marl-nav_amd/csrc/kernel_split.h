@@ -725,6 +725,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             __syncthreads();
             STAMP(4);
             if (wib == 0) {
+                if (MARLNAV_SPLIT_ENV_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_SPLIT_ENV_PRIO);
                 // every row of the workgroup: its reward terms (one lane per
                 // row, all 64 lanes busy where the row leaders were 1 in LPR)
                 static_assert(kWavesPerBlock * R <= 64, "one lane per row of the workgroup");
@@ -759,6 +760,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 c_col = __popcll(__ballot(co_l));
                 c_tar = __popcll(__ballot(ta_l));
                 STAMPX(1);
+                if (MARLNAV_SPLIT_ENV_PRIO) __builtin_amdgcn_s_setprio(0);
             } else if constexpr (kSplitOverlap<A, O>) {
                 if (ovl) {
                     // the finished set from the parked inputs (the same tests

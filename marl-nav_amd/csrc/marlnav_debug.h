@@ -67,3 +67,12 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_ENV_PRIO
 #define MARLNAV_ENV_PRIO 3
 #endif
+// A/B builds: the split kernel's wave-0 per-env phase / the env-block
+// kernel's re-init pass (waves 1..A-1 of blocks with finished envs) at this
+// s_setprio
+#ifndef MARLNAV_SPLIT_ENV_PRIO
+#define MARLNAV_SPLIT_ENV_PRIO 0
+#endif
+#ifndef MARLNAV_TAIL_PRIO
+#define MARLNAV_TAIL_PRIO 0
+#endif
