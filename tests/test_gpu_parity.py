@@ -1332,3 +1332,39 @@ def test_fused_normalizer_every_store_path(pkg, P, A, O):
         ref = (obs._packed - mean) / scale
         torch.testing.assert_close(obs._normalized, ref, rtol=0, atol=0,
                                    msg=f"P{P} A{A} O{O} step {k + 1}")
+
+
+@pytest.mark.parametrize("first,n", [
+    (0x00000000, 1 << 20),            # +0 and the smallest magnitudes
+    (0x3EFF0000, 1 << 18),            # around |x| = 0.5 (the branch point)
+    (0x3F7C0000, (1 << 18) + 1),      # the last 2^18 floats below 1, and 1
+    (0x80000000, 1 << 16),            # -0 and tiny negatives
+    (0xBF7E0000, (1 << 17) + 1),      # down to -1
+])
+def test_kernel_acos_equals_oracle_restatement(pkg, first, n):
+    """The step kernels' bearing acos (acos_k through marlnav_debug_acos_range)
+    equals the oracle's acos_device bit for bit on contiguous runs of fp32
+    inputs (environment.py:286). tests/golden/acos_dev_check.py sweeps all
+    2 130 706 434 inputs in [-1, 1] (profiles/r04_acos_device.json)."""
+    lib = pkg.abi.load_library()
+    out = torch.empty(n, dtype=torch.float32, device=DEV)
+    assert lib.marlnav_debug_acos_range(first, n, out.data_ptr(), None) == 0
+    got = np_(out)
+    exp = orc.acos_device_range(first, n)
+    bad = np.flatnonzero(got.view(np.uint32) != exp.view(np.uint32))
+    assert bad.size == 0, (f"{bad.size} of {n} differ, first at bits "
+                           f"{first + int(bad[0]):#010x}: {got[bad[0]]!r} vs {exp[bad[0]]!r}")
+
+
+def test_kernel_acos_strided_sample(pkg):
+    """Every 997th fp32 of [-1, 1] through the kernels' acos vs the oracle's."""
+    lib = pkg.abi.load_library()
+    step = 997
+    for base in (0, 0x80000000):
+        bits = np.arange(base, base + 0x3F800001, step, dtype=np.uint64).astype(np.uint32)
+        exp = orc.acos_device(bits.view(np.float32))
+        n = int(bits[-1] - bits[0]) + 1
+        out = torch.empty(n, dtype=torch.float32, device=DEV)
+        assert lib.marlnav_debug_acos_range(int(bits[0]), n, out.data_ptr(), None) == 0
+        got = np_(out[::step])
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
