@@ -78,7 +78,10 @@ __device__ __forceinline__ void out_st4(float *p, float4 v)
 constexpr int kCpolOut = MARLNAV_CPOL < 0 ? 0 : MARLNAV_CPOL;
 constexpr bool kWtOut = MARLNAV_CPOL >= 0;
 constexpr uint32_t kWriteThroughFlag = 1u << 29;  // internal MarlnavParams.flags bit
-constexpr int64_t kWriteThroughMinBytes = 8 << 20;
+#ifndef MARLNAV_WT_MIN_MB
+#define MARLNAV_WT_MIN_MB 8
+#endif
+constexpr int64_t kWriteThroughMinBytes = (int64_t)MARLNAV_WT_MIN_MB << 20;
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v2i_t __attribute__((ext_vector_type(2)));
 

@@ -76,3 +76,7 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_TAIL_PRIO
 #define MARLNAV_TAIL_PRIO 0
 #endif
+// Env-block kernel: early_out (A/B builds, kernel_block.h)
+#ifndef MARLNAV_EARLY_OUT
+#define MARLNAV_EARLY_OUT 0
+#endif
