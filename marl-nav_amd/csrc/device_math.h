@@ -70,6 +70,10 @@ __device__ __forceinline__ void out_st4(float *p, float4 v)
 // 65536x3x3 (14 MB) 8.38 -> 7.84 and 8.52 -> 8.19 us, 4096x16x32 (27 MB)
 // 13.97 -> 13.13 and 13.89 -> 13.68, 512x16x32 (3.3 MB) 9.17 -> 9.66, 8192x3x3
 // (1.8 MB) 5.57 -> 5.73, 16384x3x3 (3.5 MB) 5.82 -> 5.62 and 5.78 -> 5.80).
+// Round 4, this round's kernels, one box (profiles/r04_ab_wt.txt): threshold
+// 8 -> 2 MB: 16384x3x3 5.33 -> 5.17 us, 32768x3x3 6.23 -> 5.91, 512x16x32
+// 8.31 -> 8.06, 1024x16x32 8.85 -> 8.38; 8192x3x3 (1.8 MB) stays at 5.05
+// below it (5.11 written through); 0 MB would take 2x3x3 3.01 -> 3.11.
 // marlnav_step / marlnav_observe set kWriteThroughFlag in
 // MarlnavParams.flags; `wt` in the kernels is that bit.
 #ifndef MARLNAV_CPOL
@@ -79,7 +83,7 @@ constexpr int kCpolOut = MARLNAV_CPOL < 0 ? 0 : MARLNAV_CPOL;
 constexpr bool kWtOut = MARLNAV_CPOL >= 0;
 constexpr uint32_t kWriteThroughFlag = 1u << 29;  // internal MarlnavParams.flags bit
 #ifndef MARLNAV_WT_MIN_MB
-#define MARLNAV_WT_MIN_MB 8
+#define MARLNAV_WT_MIN_MB 2
 #endif
 constexpr int64_t kWriteThroughMinBytes = (int64_t)MARLNAV_WT_MIN_MB << 20;
 typedef int v4i_t __attribute__((ext_vector_type(4)));

@@ -594,6 +594,8 @@ __global__ void __launch_bounds__(64 * A)
             }
         }
         const int nfin = flg[0];
+        if (kDeferReinitOut && nfin && overlap && !(MARLNAV_AB & 1))  // the re-init's obstacles and targets
+            store_reinit_out<A, O>(kargs_late<kHotKargsOff>(), ev, list, nfin, tid, NT);
         if (nfin && !overlap) {
             // ---- reference-RNG / noisy re-init (:104; noisy: done above by
             // wave 0) and observations of the re-initialised envs (:105)

@@ -401,6 +401,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     b.step_num = const_cast<float *>(h_step_num);
     b.terminates = const_cast<uint8_t *>(h_terminates);
     STAMP(0);
+    if (MARLNAV_AB & 4096) return;  // (AB 4096: timing only - the launch alone)
     float *wl = lds + wib * SP::FLOATS;
     float *st = wl + SP::ST;
     const int64_t e0 = tile * EPW;
@@ -471,6 +472,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
     wave_sync();
     STAMP(1);
+    if (MARLNAV_AB & 8192) return;  // (AB 8192: timing only - staged, then exit)
 
     // kSplitTpl (native re-init): the formation and its observation template
     // (NCP floats) into registers now, a few per thread, so their loads run
@@ -621,6 +623,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         // reward rows `red` (A float4: r_miss, r_hit, flags), step number and
         // `terminates` in); returns fin and sets the counter flags
         bool tr_l = false, co_l = false, ta_l = false;
+        // workgroup-spread shapes: wave 0's five per-env stores wait until
+        // after the per-env barrier (kSplitDeferEnvOut), so that they do not
+        // hold wave 0 - and the workgroup at that barrier - at issue behind
+        // the other workgroups' tile stores in the CU's vector-memory path
+        constexpr bool kDeferEnv = kSplitSpread<A, O> && MARLNAV_SPLIT_DEFER_ENV_OUT;
+        float dv_rew = 0.0f, dv_sn = 0.0f;
+        unsigned dv_fl = 0u;
+        bool dv_on = false;
         const auto per_env = [&](int64_t e, const float4 *red, float sn_v, unsigned term_v,
                                  float *s5, float *obl, float *tgl) -> bool {
             unsigned any_col = 0u, all_in = 1u;
@@ -638,14 +648,18 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 #pragma unroll
             for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
             const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
-            out_el(b.reward, e, rsum / (float)A);             // torch.mean (:233)
+            dv_rew = rsum / (float)A;                          // torch.mean (:233)
+            if (!kDeferEnv) out_el(b.reward, e, dv_rew);
             float step_num = sn_v + 1.0f;                      // :96
             const bool truncated = step_num > pr.trunc_after;  // :97
             const bool term_old = term_v != 0u;
             const bool terminated = any_col || term_old;       // :213-214
-            out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
-            out_el(b.terminated, e, (uint8_t)terminated);
-            out_el(b.truncated, e, (uint8_t)truncated);
+            dv_fl = (!term_old && all_in ? 1u : 0u) | (terminated ? 2u : 0u) | (truncated ? 4u : 0u);
+            if (!kDeferEnv) {
+                out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
+                out_el(b.terminated, e, (uint8_t)terminated);
+                out_el(b.truncated, e, (uint8_t)truncated);
+            }
             const bool fin = truncated || terminated;          // :102-104
             if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
                 KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -680,7 +694,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 out_el(gtg, 2 * e + 1, tgl[1]);
             }
             if (fin) step_num = blend_in(step_num, 0.0f);
-            out_el(b.step_num, e, step_num);
+            dv_sn = step_num;
+            dv_on = true;
+            if (!kDeferEnv) out_el(b.step_num, e, step_num);
             tr_l = truncated;
             co_l = any_col;
             ta_l = all_in;
@@ -724,6 +740,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             }
             __syncthreads();
             STAMP(4);
+            if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
             if (wib == 0) {
                 if (MARLNAV_SPLIT_ENV_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_SPLIT_ENV_PRIO);
                 // every row of the workgroup: its reward terms (one lane per
@@ -785,6 +802,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             }
             __syncthreads();
             STAMPX(2);
+            if (kDeferEnv && wib == 0 && dv_on) {  // wave 0's per-env outputs (above)
+                const int64_t e = blk0 * EPW + (int)lane;
+                out_el(b.reward, e, dv_rew);
+                out_el(b.terminates, e, (uint8_t)(dv_fl & 1u));
+                out_el(b.terminated, e, (uint8_t)((dv_fl >> 1) & 1u));
+                out_el(b.truncated, e, (uint8_t)((dv_fl >> 2) & 1u));
+                out_el(b.step_num, e, dv_sn);
+            }
+            if (MARLNAV_AB & 32768) return;  // (AB 32768: timing only - per-env done, then exit)
             const FlatFinList list{bslot, bcnt[0]};
 #if MARLNAV_STAMPS
             stamp_nfin = list.total();
@@ -798,6 +824,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 // fused native re-init + re-observation recomputes a Philox
                 // block per obstacle pair: only for few obstacles
                 if (ovl) {  // the pass ran above
+                    if (kDeferReinitOut) store_reinit_out<A, O>(kl, ev, list, nfin, tid, nt);
                     if (*unclean) {  // an agent or target off the formation: every pair
                         reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
                         __syncthreads();
@@ -806,6 +833,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     reinit_reobs_native<A, O, SP::EW>(kl, ev, kl->a.b.formation, list, nfin,
                                                       pr.cap_distance, tid, nt, pre);
                     __syncthreads();
+                    if (kDeferReinitOut) store_reinit_out<A, O>(kl, ev, list, nfin, tid, nt);
                 } else if (kSplitTplPass<A, O> && tpl_on && live == kWavesPerBlock) {
                     if constexpr (kSplitTplPass<A, O>) {
                         // one pass (formation and template parked by every wave)
@@ -815,6 +843,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                             nfin, pr.cap_distance, tid, unclean);
                         __syncthreads();
                         STAMPX(3);
+                        if (kDeferReinitOut) store_reinit_out<A, O>(kl, ev, list, nfin, tid, nt);
                         if (*unclean) {  // an agent or target off the formation: every pair
                             reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
                             __syncthreads();
@@ -869,6 +898,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 
     // ---- stream the tile out (obs rows and states from LDS)
     wave_sync();
+    if (MARLNAV_AB & 2) return;  // (AB 2: timing only - no store)
     {
         const float *src = wl + SP::OBS;
         float *gobs = in_sgpr(b.obs + e0 * (A * D));

@@ -80,3 +80,9 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_EARLY_OUT
 #define MARLNAV_EARLY_OUT 0
 #endif
+// Split kernel, workgroup-spread shapes: wave 0's per-env stores after the
+// per-env barrier (1, A/B builds: no change at 4096x16x32, 11.96 vs 11.97 us)
+// or inside the per-env phase (0)
+#ifndef MARLNAV_SPLIT_DEFER_ENV_OUT
+#define MARLNAV_SPLIT_DEFER_ENV_OUT 0
+#endif
