@@ -430,6 +430,9 @@ __global__ void __launch_bounds__(64 * A)
     // block's finished envs.
     const bool early_out = MARLNAV_EARLY_OUT && !OBS_ONLY && !NOISY && full && !norm &&
                            !K->a.b.fresh_states;
+    // defer_env: wave 0's per-env stores and counter atomics after the
+    // per-env barrier (with early_out, or alone: MARLNAV_DEFER_BLOCK_ENV_OUT)
+    const bool defer_env = early_out || (MARLNAV_DEFER_BLOCK_ENV_OUT && !OBS_ONLY && !NOISY);
     uint64_t fin_blk = 0ull;
     float d_rew = 0.0f, d_sn = 0.0f;  // wave 0's deferred per-env outputs
     unsigned d_fl = 0u, d_cnt = 0u;
@@ -461,7 +464,7 @@ __global__ void __launch_bounds__(64 * A)
                 STAMPX(0);  // (wave 0: the reward terms read)
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
                 d_rew = rsum / (float)A;                           // torch.mean (:233)
-                if (!(MARLNAV_AB & 1024) && !early_out)  // (AB 1024: timing only, no per-env stores)
+                if (!(MARLNAV_AB & 1024) && !defer_env)  // (AB 1024: timing only, no per-env stores)
                 out_el(b.reward, e, d_rew);
 
                 float step_num = lds[BP::SN + l] + 1.0f;           // :96
@@ -469,7 +472,7 @@ __global__ void __launch_bounds__(64 * A)
                 const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
                 const bool terminated = any_col || term_old;       // :213-214
                 d_fl = (!term_old && all_in ? 1u : 0u) | (terminated ? 2u : 0u) | (truncated ? 4u : 0u);
-                if (!(MARLNAV_AB & 1024) && !early_out) {
+                if (!(MARLNAV_AB & 1024) && !defer_env) {
                 out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
                 out_el(b.terminated, e, (uint8_t)terminated);
                 out_el(b.truncated, e, (uint8_t)truncated);
@@ -501,7 +504,7 @@ __global__ void __launch_bounds__(64 * A)
                 }
                 d_sn = fin ? blend_in(step_num, 0.0f) : step_num;
                 d_on = true;
-                if (!(MARLNAV_AB & 1024) && !early_out)
+                if (!(MARLNAV_AB & 1024) && !defer_env)
                 out_el(b.step_num, e, d_sn);
                 tr_l = truncated;
                 co_l = any_col;
@@ -519,7 +522,7 @@ __global__ void __launch_bounds__(64 * A)
             d_cnt = c_trunc | (c_col << 8) | (c_tar << 16);
             if (lane == 0) {
                 flg[0] = (int)__popcll(finmask);
-                if ((c_trunc | c_col | c_tar) && !(MARLNAV_AB & 512) && !early_out) {  // (AB 512: timing only)
+                if ((c_trunc | c_col | c_tar) && !(MARLNAV_AB & 512) && !defer_env) {  // (AB 512: timing only)
                     KArgsK *kl = kargs_late<kHotKargsOff>();
                     uint64_t *cnt = kl->a.b.counters;
                     const int64_t slots = kl->a.waves;
@@ -570,7 +573,7 @@ __global__ void __launch_bounds__(64 * A)
         }
         __syncthreads();
         STAMP(4);
-        if (early_out && w == 0) {  // wave 0's per-env outputs and counters
+        if (defer_env && w == 0) {  // wave 0's per-env outputs and counters
             if (d_on && !(MARLNAV_AB & 1024)) {
                 const int64_t e = e0 + l;
                 out_el(b.reward, e, d_rew);

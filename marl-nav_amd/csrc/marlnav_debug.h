@@ -86,3 +86,8 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_SPLIT_DEFER_ENV_OUT
 #define MARLNAV_SPLIT_DEFER_ENV_OUT 0
 #endif
+// Env-block kernel: wave 0's per-env stores and counter atomics after the
+// per-env barrier (A/B builds)
+#ifndef MARLNAV_DEFER_BLOCK_ENV_OUT
+#define MARLNAV_DEFER_BLOCK_ENV_OUT 0
+#endif
