@@ -110,6 +110,14 @@ constexpr bool kSplitTplPass = kSplitTpl<A, O> && (64 * kWavesPerBlock) % O == 0
 // and the per-env phase (the A3 env-block kernel's overlap): each wave parks
 // its envs' collision bits with their step numbers and `terminates` flags, so
 // the other waves find the finished set without waiting for wave 0
+// ... and each wave finishing its own envs' row rewards and per-env phase
+// right after its observe phase (no wait for the workgroup's slowest wave,
+// no serial pass on wave 0), storing its tile at once when none of its envs
+// finished; the workgroup's finished envs then go through the one-pass
+// re-init after one barrier, and only their waves store after it
+template <int A, int O>
+constexpr bool kSplitOwnEnv = kSplitTplPass<A, O> && !kSplitRRLeader<A, O> && MARLNAV_SPLIT_OWN_ENV;
+
 template <int A, int O>
 constexpr bool kSplitOverlap = kSplitTplPass<A, O> && !kSplitRRLeader<A, O> &&
                                (64 * (kWavesPerBlock - 1)) % O == 0 && MARLNAV_SPLIT_OVERLAP;
@@ -617,6 +625,109 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     }
     STAMP(3);
 
+    // ---- the tile's rows and states from LDS to global memory (at the
+    // end of the step, or - kSplitOwnEnv - as soon as none of the wave's
+    // envs finished)
+    const auto store_tile = [&]() {
+        {
+            const float *src = wl + SP::OBS;
+            float *gobs = in_sgpr(b.obs + e0 * (A * D));
+            const int n = nr * D;
+            constexpr int VAL = gcd_c(R * D * 4, 16);  // tile base alignment in bytes
+            float *gnorm = nullptr;
+            const float *mean = nullptr, *scale = nullptr;
+            if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
+                KArgsK *kl = kargs_late<kHotKargsOff>();
+                gnorm = kl->a.b.obs_norm + e0 * (A * D);
+                mean = kl->a.b.norm_mean;
+                scale = kl->a.b.norm_scale;
+            }
+            if constexpr (SP::DP != D) {  // padded rows (D % 4 == 0): 16-byte pieces
+                static_assert(D % 4 == 0 && SP::DP % 4 == 0, "padded rows keep 16-byte alignment");
+                constexpr int D4 = D / 4;
+                if (VAL % 16 == 0) {
+                    for (int i = (int)lane; i < n / 4; i += 64) {
+                        const int rr = i / D4, c4 = i - rr * D4;
+                        // (AB 2048: timing only - consecutive pieces, no bank
+                        // conflicts: the most an XOR swizzle of the pieces can save)
+                        const float4 v = *reinterpret_cast<const float4 *>(
+                            (MARLNAV_AB & 2048) ? src + 4 * i : src + rr * SP::DP + 4 * c4);
+                        if (kWtOut && wt)
+                            wt_st4(out_buf(gobs, 4u * n), 16u * i, v);
+                        else
+                            out_st4<kNtRows>(gobs + 4 * i, v);
+                    }
+                } else {
+                    for (int i = (int)lane; i < n; i += 64) {
+                        const int rr = i / D;
+                        const float v = src[rr * SP::DP + (i - rr * D)];
+                        if (kWtOut && wt)
+                            wt_st(out_buf(gobs, 4u * n), 4u * i, v);
+                        else
+                            out_st<kNtRows>(gobs + i, v);
+                    }
+                }
+            } else if (VAL % 16 == 0 && ne == EPW) {
+                for (int i = (int)lane; i < n / 4; i += 64) {
+                    const float4 v = reinterpret_cast<const float4 *>(src)[i];
+                    if (kWtOut && wt)
+                        wt_st4(out_buf(gobs, 4u * n), 16u * i, v);
+                    else
+                        out_st4<kNtRows>(gobs + 4 * i, v);
+                }
+            } else if (VAL % 8 == 0 && n % 2 == 0) {
+                for (int i = (int)lane; i < n / 2; i += 64) {
+                    const float2 v = reinterpret_cast<const float2 *>(src)[i];
+                    if (kWtOut && wt)
+                        wt_st2(out_buf(gobs, 4u * n), 8u * i, v);
+                    else
+                        out_st2<kNtRows>(gobs + 2 * i, v);
+                }
+            } else {
+                for (int i = (int)lane; i < n; i += 64) {
+                    if (kWtOut && wt)
+                        wt_st(out_buf(gobs, 4u * n), 4u * i, src[i]);
+                    else
+                        out_st<kNtRows>(gobs + i, src[i]);
+                }
+            }
+            if (gnorm) {
+                const OutBuf nb = out_buf(gnorm, 4u * n);
+    #pragma unroll 8  // (mean/scale loads of 8 iterations in flight at once)
+                for (int i = (int)lane; i < n; i += 64) {
+                    const int rr = i / D, kk = i - rr * D;
+                    const float v = (src[rr * SP::DP + kk] - mean[kk]) / scale[kk];
+                    if (kWtOut && wt)
+                        wt_st(nb, 4u * i, v);
+                    else
+                        gnorm[i] = v;
+                }
+            }
+        }
+        if (!OBS_ONLY) {
+            float *gst = in_sgpr(b.states_out + e0 * (A * 5));
+            const int n = nr * 5;
+            constexpr int SAL = gcd_c(R * 20, 16);
+            if (SAL % 16 == 0 && ne == EPW) {
+                for (int i = (int)lane; i < n / 4; i += 64) {
+                    const float4 v = reinterpret_cast<const float4 *>(st)[i];
+                    if (kWtOut && wt)
+                        wt_st4(out_buf(gst, 4u * n), 16u * i, v);
+                    else
+                        out_st4<kNtRows>(gst + 4 * i, v);
+                }
+            } else {
+                for (int i = (int)lane; i < n; i += 64) {
+                    if (kWtOut && wt)
+                        wt_st(out_buf(gst, 4u * n), 4u * i, st[i]);
+                    else
+                        out_st<kNtRows>(gst + i, st[i]);
+                }
+            }
+        }
+    };
+    bool own_done = false;  // this wave's tile already stored (kSplitOwnEnv)
+
     if (!OBS_ONLY) {
         wave_sync();
         // ---- per-env reductions, terminal logic, masked re-init (env e,
@@ -728,6 +839,36 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     if (idx < SP::NCP) ftp[idx] = cp[k2];
                 }
             }
+            // kSplitOwnEnv (full workgroups with the formation template)
+            const bool own = kSplitOwnEnv<A, O> && !NOISY && tpl_on && live == kWavesPerBlock;
+            if (own) {
+                if ((int)lane < nr) {  // this wave's rows: their reward terms
+                    float4 *rp = reinterpret_cast<float4 *>(wl + SP::RED) + lane;
+                    const float4 tv = *rp;
+                    *rp = row_reward(tv.x, tv.y, __float_as_uint(tv.z), __float_as_int(tv.w),
+                                     wl + SP::BOND + (int)lane * (A - 1));
+                }
+                wave_sync();
+                bool fin = false;
+                if (env_on)
+                    fin = per_env(e0 + lane, reinterpret_cast<const float4 *>(wl + SP::RED) + A * lane,
+                                  sn_in, term_in, st + 5 * A * lane, wl + SP::OB + 2 * O * lane,
+                                  wl + SP::TG + 2 * lane);
+                const uint64_t fm = __ballot(fin);
+                if (fin)  // SplitFinList: env codes wib * EPW + env
+                    bslot[wib * EPW + (int)__builtin_amdgcn_mbcnt_hi(
+                                          (unsigned)(fm >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] =
+                        wib * EPW + (int)lane;
+                if (lane == 0) bcnt[wib] = (int)__popcll(fm);
+                c_trunc = __popcll(__ballot(tr_l));
+                c_col = __popcll(__ballot(co_l));
+                c_tar = __popcll(__ballot(ta_l));
+                if (fm == 0ull && !(MARLNAV_AB & 2)) {
+                    store_tile();
+                    own_done = true;
+                }
+            }
             if (env_on) {
                 bsn[wib * EPW + (int)lane] = sn_in;
                 bterm[wib * EPW + (int)lane] = term_in;
@@ -741,6 +882,27 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             __syncthreads();
             STAMP(4);
             if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
+            if constexpr (kSplitOwnEnv<A, O>) {
+                if (own) {
+                    const SplitFinList<EPW> olist = SplitFinList<EPW>::make(bcnt, bslot, live);
+                    if (const int nfin = (MARLNAV_AB & 1) ? 0 : olist.total()) {
+                        KArgsK *kl = kargs_late<kHotKargsOff>();
+                        const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP>
+                            ev{lds, blk0 * EPW};
+                        const float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
+                        const int tid = (int)threadIdx.x, nt = 64 * kWavesPerBlock;
+                        reinit_reobs_tpl<A, O, 64 * kWavesPerBlock>(
+                            kl, ev, ftp, reinterpret_cast<const float2 *>(ftp + SP::NF), olist,
+                            nfin, pr.cap_distance, tid, unclean);
+                        __syncthreads();
+                        if (*unclean) {  // an agent or target off the formation: every pair
+                            reobs_block<A, O>(ev, olist, nfin, pr.cap_distance, tid, nt);
+                            __syncthreads();
+                        }
+                    }
+                }
+            }
+            if (!own) {  // ---- wave 0's per-env phase for the whole workgroup
             if (wib == 0) {
                 if (MARLNAV_SPLIT_ENV_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_SPLIT_ENV_PRIO);
                 // every row of the workgroup: its reward terms (one lane per
@@ -859,6 +1021,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     __syncthreads();
                 }
             }
+            }  // (!own)
         } else {
             bool fin = false;
             if (env_on)
@@ -899,102 +1062,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     // ---- stream the tile out (obs rows and states from LDS)
     wave_sync();
     if (MARLNAV_AB & 2) return;  // (AB 2: timing only - no store)
-    {
-        const float *src = wl + SP::OBS;
-        float *gobs = in_sgpr(b.obs + e0 * (A * D));
-        const int n = nr * D;
-        constexpr int VAL = gcd_c(R * D * 4, 16);  // tile base alignment in bytes
-        float *gnorm = nullptr;
-        const float *mean = nullptr, *scale = nullptr;
-        if (!OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM)) {
-            KArgsK *kl = kargs_late<kHotKargsOff>();
-            gnorm = kl->a.b.obs_norm + e0 * (A * D);
-            mean = kl->a.b.norm_mean;
-            scale = kl->a.b.norm_scale;
-        }
-        if constexpr (SP::DP != D) {  // padded rows (D % 4 == 0): 16-byte pieces
-            static_assert(D % 4 == 0 && SP::DP % 4 == 0, "padded rows keep 16-byte alignment");
-            constexpr int D4 = D / 4;
-            if (VAL % 16 == 0) {
-                for (int i = (int)lane; i < n / 4; i += 64) {
-                    const int rr = i / D4, c4 = i - rr * D4;
-                    // (AB 2048: timing only - consecutive pieces, no bank
-                    // conflicts: the most an XOR swizzle of the pieces can save)
-                    const float4 v = *reinterpret_cast<const float4 *>(
-                        (MARLNAV_AB & 2048) ? src + 4 * i : src + rr * SP::DP + 4 * c4);
-                    if (kWtOut && wt)
-                        wt_st4(out_buf(gobs, 4u * n), 16u * i, v);
-                    else
-                        out_st4<kNtRows>(gobs + 4 * i, v);
-                }
-            } else {
-                for (int i = (int)lane; i < n; i += 64) {
-                    const int rr = i / D;
-                    const float v = src[rr * SP::DP + (i - rr * D)];
-                    if (kWtOut && wt)
-                        wt_st(out_buf(gobs, 4u * n), 4u * i, v);
-                    else
-                        out_st<kNtRows>(gobs + i, v);
-                }
-            }
-        } else if (VAL % 16 == 0 && ne == EPW) {
-            for (int i = (int)lane; i < n / 4; i += 64) {
-                const float4 v = reinterpret_cast<const float4 *>(src)[i];
-                if (kWtOut && wt)
-                    wt_st4(out_buf(gobs, 4u * n), 16u * i, v);
-                else
-                    out_st4<kNtRows>(gobs + 4 * i, v);
-            }
-        } else if (VAL % 8 == 0 && n % 2 == 0) {
-            for (int i = (int)lane; i < n / 2; i += 64) {
-                const float2 v = reinterpret_cast<const float2 *>(src)[i];
-                if (kWtOut && wt)
-                    wt_st2(out_buf(gobs, 4u * n), 8u * i, v);
-                else
-                    out_st2<kNtRows>(gobs + 2 * i, v);
-            }
-        } else {
-            for (int i = (int)lane; i < n; i += 64) {
-                if (kWtOut && wt)
-                    wt_st(out_buf(gobs, 4u * n), 4u * i, src[i]);
-                else
-                    out_st<kNtRows>(gobs + i, src[i]);
-            }
-        }
-        if (gnorm) {
-            const OutBuf nb = out_buf(gnorm, 4u * n);
-#pragma unroll 8  // (mean/scale loads of 8 iterations in flight at once)
-            for (int i = (int)lane; i < n; i += 64) {
-                const int rr = i / D, kk = i - rr * D;
-                const float v = (src[rr * SP::DP + kk] - mean[kk]) / scale[kk];
-                if (kWtOut && wt)
-                    wt_st(nb, 4u * i, v);
-                else
-                    gnorm[i] = v;
-            }
-        }
-    }
-    if (!OBS_ONLY) {
-        float *gst = in_sgpr(b.states_out + e0 * (A * 5));
-        const int n = nr * 5;
-        constexpr int SAL = gcd_c(R * 20, 16);
-        if (SAL % 16 == 0 && ne == EPW) {
-            for (int i = (int)lane; i < n / 4; i += 64) {
-                const float4 v = reinterpret_cast<const float4 *>(st)[i];
-                if (kWtOut && wt)
-                    wt_st4(out_buf(gst, 4u * n), 16u * i, v);
-                else
-                    out_st4<kNtRows>(gst + 4 * i, v);
-            }
-        } else {
-            for (int i = (int)lane; i < n; i += 64) {
-                if (kWtOut && wt)
-                    wt_st(out_buf(gst, 4u * n), 4u * i, st[i]);
-                else
-                    out_st<kNtRows>(gst + i, st[i]);
-            }
-        }
-    }
+    if (!own_done) store_tile();
     STAMP(6);
     if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
         KArgsK *kl = kargs_late<kHotKargsOff>();

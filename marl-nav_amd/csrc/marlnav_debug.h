@@ -91,3 +91,8 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_DEFER_BLOCK_ENV_OUT
 #define MARLNAV_DEFER_BLOCK_ENV_OUT 0
 #endif
+// Split kernel, kSplitTplPass shapes: each wave's own row rewards and
+// per-env phase before the workgroup barrier (kSplitOwnEnv)
+#ifndef MARLNAV_SPLIT_OWN_ENV
+#define MARLNAV_SPLIT_OWN_ENV 0
+#endif
