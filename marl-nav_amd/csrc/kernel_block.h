@@ -139,54 +139,6 @@ __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float
         if ((k + 1) * NT <= Q2 || tid + k * NT < Q2) out_st4<kNtRows>(d2 + 4 * (tid + k * NT), v2[k]);
 }
 
-// block_store2 of the 16-byte pieces that touch a finished env of the block
-// (bit l of fin: env l; G1 / G2 floats per env in span 1 / 2), or with
-// FIN = false of the pieces that touch none. The two calls together store
-// every piece once.
-template <int N1, int N2, int NT, int G1, int G2, bool FIN>
-__device__ __forceinline__ void block_store2_env(float *__restrict__ d1, const float *__restrict__ s1,
-                                                 float *__restrict__ d2, const float *__restrict__ s2,
-                                                 int tid, bool wt, uint64_t fin)
-{
-    static_assert(N1 % 4 == 0 && N2 % 4 == 0, "whole 16-byte pieces");
-    constexpr int Q1 = N1 / 4, Q2 = N2 / 4, K1 = (Q1 + NT - 1) / NT, K2 = (Q2 + NT - 1) / NT;
-    auto pick = [fin](int q, int g) {
-        const bool touch = (((fin >> (4 * q / g)) | (fin >> ((4 * q + 3) / g))) & 1ull) != 0ull;
-        return touch == FIN;
-    };
-    float4 v1[K1], v2[K2];
-    bool p1[K1], p2[K2];
-#pragma unroll
-    for (int k = 0; k < K1; ++k) {
-        const int q = tid + k * NT;
-        p1[k] = ((k + 1) * NT <= Q1 || q < Q1) && pick(q, G1);
-        if (p1[k]) v1[k] = reinterpret_cast<const float4 *>(s1)[q];
-    }
-#pragma unroll
-    for (int k = 0; k < K2; ++k) {
-        const int q = tid + k * NT;
-        p2[k] = ((k + 1) * NT <= Q2 || q < Q2) && pick(q, G2);
-        if (p2[k]) v2[k] = reinterpret_cast<const float4 *>(s2)[q];
-    }
-    if (kWtOut && wt) {
-        const OutBuf o1 = out_buf(d1, N1 * 4), o2 = out_buf(d2, N2 * 4);
-#pragma unroll
-        for (int k = 0; k < K1; ++k)
-            if (p1[k]) wt_st4(o1, 16u * (tid + k * NT), v1[k]);
-#pragma unroll
-        for (int k = 0; k < K2; ++k)
-            if (p2[k]) wt_st4(o2, 16u * (tid + k * NT), v2[k]);
-        return;
-    }
-#pragma unroll
-    for (int k = 0; k < K1; ++k)
-        if (p1[k]) out_st4<kNtRows>(d1 + 4 * (tid + k * NT), v1[k]);
-#pragma unroll
-    for (int k = 0; k < K2; ++k)
-        if (p2[k]) out_st4<kNtRows>(d2 + 4 * (tid + k * NT), v2[k]);
-}
-
-
 // Phases (one block barrier after each of the first four): stage | move +
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
@@ -422,21 +374,6 @@ __global__ void __launch_bounds__(64 * A)
     float *gobs = in_sgpr(b.obs + e0 * (A * D));
     if (OBS_ONLY) block_store(gobs, obs_rows, nrow * D, tid, NT, wt);
     const bool norm = !OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM);
-    // early_out (MARLNAV_EARLY_OUT, A/B builds): the unfinished envs' rows and
-    // states leave from waves 1..A-1 as soon as the finished set is known,
-    // under wave 0's per-env phase, whose own stores and counter atomics
-    // wait until after the barrier (so they do not queue behind that burst);
-    // the finished envs' pieces leave after their re-init. fin_blk: the
-    // block's finished envs.
-    const bool early_out = MARLNAV_EARLY_OUT && !OBS_ONLY && !NOISY && full && !norm &&
-                           !K->a.b.fresh_states;
-    // defer_env: wave 0's per-env stores and counter atomics after the
-    // per-env barrier (with early_out, or alone: MARLNAV_DEFER_BLOCK_ENV_OUT)
-    const bool defer_env = early_out || (MARLNAV_DEFER_BLOCK_ENV_OUT && !OBS_ONLY && !NOISY);
-    uint64_t fin_blk = 0ull;
-    float d_rew = 0.0f, d_sn = 0.0f;  // wave 0's deferred per-env outputs
-    unsigned d_fl = 0u, d_cnt = 0u;
-    bool d_on = false;
     if (!OBS_ONLY) {
         int *list = reinterpret_cast<int *>(lds + BP::LIST);
         int *flg = reinterpret_cast<int *>(lds + BP::FLG);
@@ -463,16 +400,14 @@ __global__ void __launch_bounds__(64 * A)
                 for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
                 STAMPX(0);  // (wave 0: the reward terms read)
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
-                d_rew = rsum / (float)A;                           // torch.mean (:233)
-                if (!(MARLNAV_AB & 1024) && !defer_env)  // (AB 1024: timing only, no per-env stores)
-                out_el(b.reward, e, d_rew);
+                if (!(MARLNAV_AB & 1024))  // (AB 1024: timing only, no per-env stores)
+                out_el(b.reward, e, rsum / (float)A);              // torch.mean (:233)
 
                 float step_num = lds[BP::SN + l] + 1.0f;           // :96
                 const bool truncated = step_num > pr.trunc_after;  // :97
                 const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
                 const bool terminated = any_col || term_old;       // :213-214
-                d_fl = (!term_old && all_in ? 1u : 0u) | (terminated ? 2u : 0u) | (truncated ? 4u : 0u);
-                if (!(MARLNAV_AB & 1024) && !defer_env) {
+                if (!(MARLNAV_AB & 1024)) {
                 out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
                 out_el(b.terminated, e, (uint8_t)terminated);
                 out_el(b.truncated, e, (uint8_t)truncated);
@@ -502,27 +437,23 @@ __global__ void __launch_bounds__(64 * A)
                         out_el(kl->a.b.target, 2 * e + 1, tgl[1]);
                     }
                 }
-                d_sn = fin ? blend_in(step_num, 0.0f) : step_num;
-                d_on = true;
-                if (!(MARLNAV_AB & 1024) && !defer_env)
-                out_el(b.step_num, e, d_sn);
+                if (!(MARLNAV_AB & 1024))
+                out_el(b.step_num, e, fin ? blend_in(step_num, 0.0f) : step_num);
                 tr_l = truncated;
                 co_l = any_col;
                 ta_l = all_in;
             }
             STAMPX(1);  // (wave 0: the per-env outputs issued)
             const uint64_t finmask = __ballot(fin);
-            fin_blk = finmask;
             if (fin)
                 list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
                                                __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] = l;
             const unsigned c_trunc = __popcll(__ballot(tr_l));
             const unsigned c_col = __popcll(__ballot(co_l));
             const unsigned c_tar = __popcll(__ballot(ta_l));
-            d_cnt = c_trunc | (c_col << 8) | (c_tar << 16);
             if (lane == 0) {
                 flg[0] = (int)__popcll(finmask);
-                if ((c_trunc | c_col | c_tar) && !(MARLNAV_AB & 512) && !defer_env) {  // (AB 512: timing only)
+                if ((c_trunc | c_col | c_tar) && !(MARLNAV_AB & 512)) {  // (AB 512: timing only)
                     KArgsK *kl = kargs_late<kHotKargsOff>();
                     uint64_t *cnt = kl->a.b.counters;
                     const int64_t slots = kl->a.waves;
@@ -551,18 +482,8 @@ __global__ void __launch_bounds__(64 * A)
                       reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
             }
             const uint64_t fm = __ballot(fin);
-            fin_blk = fm;
             STAMPX(0);
-            if (early_out && !(MARLNAV_AB & 2)) {
-                float *gst = in_sgpr(b.states_out + e0 * (A * 5));
-                if (fm == 0ull)
-                    block_store2<E * A * D, E * A * 5, NT - 64>(gobs, obs_rows, gst, st, tid - 64, wt);
-                else
-                    block_store2_env<E * A * D, E * A * 5, NT - 64, A * D, A * 5, false>(
-                        gobs, obs_rows, gst, st, tid - 64, wt, fm);
-            }
             if (fm && !(MARLNAV_AB & 1)) {
-                if (MARLNAV_TAIL_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_TAIL_PRIO);  // (A/B builds)
                 STAMPX(1);
                 reinit_reobs_native<A, O, kPre ? E : 0>(kargs_late<kHotKargsOff>(), ev,
                                                         lds + BP::FORM, MaskList{fm},
@@ -573,32 +494,7 @@ __global__ void __launch_bounds__(64 * A)
         }
         __syncthreads();
         STAMP(4);
-        if (defer_env && w == 0) {  // wave 0's per-env outputs and counters
-            if (d_on && !(MARLNAV_AB & 1024)) {
-                const int64_t e = e0 + l;
-                out_el(b.reward, e, d_rew);
-                out_el(b.terminates, e, (uint8_t)(d_fl & 1u));
-                out_el(b.terminated, e, (uint8_t)((d_fl >> 1) & 1u));
-                out_el(b.truncated, e, (uint8_t)((d_fl >> 2) & 1u));
-                out_el(b.step_num, e, d_sn);
-            }
-            const unsigned c_trunc = d_cnt & 0xffu, c_col = (d_cnt >> 8) & 0xffu,
-                           c_tar = d_cnt >> 16;
-            if (lane == 0 && d_cnt && !(MARLNAV_AB & 512)) {
-                KArgsK *kl = kargs_late<kHotKargsOff>();
-                uint64_t *cnt = kl->a.b.counters;
-                const int64_t slots = kl->a.waves;
-                if (cnt) {
-                    const int64_t sl = blk < slots ? blk : blk % slots;
-                    if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
-                    if (c_col) atomicAdd((unsigned long long *)&cnt[1 * slots + sl], (unsigned long long)c_col);
-                    if (c_tar) atomicAdd((unsigned long long *)&cnt[2 * slots + sl], (unsigned long long)c_tar);
-                }
-            }
-        }
         const int nfin = flg[0];
-        if (kDeferReinitOut && nfin && overlap && !(MARLNAV_AB & 1))  // the re-init's obstacles and targets
-            store_reinit_out<A, O>(kargs_late<kHotKargsOff>(), ev, list, nfin, tid, NT);
         if (nfin && !overlap) {
             // ---- reference-RNG / noisy re-init (:104; noisy: done above by
             // wave 0) and observations of the re-initialised envs (:105)
@@ -611,11 +507,7 @@ __global__ void __launch_bounds__(64 * A)
         }
     }
     STAMP(5);
-    if (early_out) {  // ---- the finished envs' pieces (the rest left above)
-        if (fin_blk && !(MARLNAV_AB & 2))
-            block_store2_env<E * A * D, E * A * 5, NT, A * D, A * 5, true>(
-                gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)), st, tid, wt, fin_blk);
-    } else if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
+    if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
         if (!(MARLNAV_AB & 2))
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)),
                                                st, tid, wt);  // (E = 64: whole 16-byte pieces)

@@ -287,17 +287,6 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
 // runs both code paths one after the other (the pass is the tail of the
 // block: issue-bound on the few waves that have items). A wave with no item
 // left skips the pass. `tid` and `nt` are wave-aligned.
-// 1 (A/B builds): native re-init passes leave the fresh obstacles and
-// targets in LDS only and the caller stores them after the pass
-// (store_reinit_out). Measured slower (graph replay, profiles/r04_ab_defer.txt):
-// 65536x3x3 6.98 -> 7.18 us, 16384x3x3 5.30 -> 5.49, 4096x16x32 11.79 ->
-// 11.96, 1024x3x8 4.96 -> 5.17 - the stores inside the pass are not what
-// holds it up, and the extra loop after its barrier is on the tail's path.
-#ifndef MARLNAV_DEFER_REINIT_OUT
-#define MARLNAV_DEFER_REINIT_OUT 0
-#endif
-constexpr bool kDeferReinitOut = MARLNAV_DEFER_REINIT_OUT != 0;
-
 template <int A, int O>
 struct NativeItems {
     static constexpr int NP = 1 + O + (A - 1), NB = (O + 1) / 2;
@@ -391,7 +380,7 @@ __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, con
         float *d = ev.targ(c) + j;
         const float v = blend_in(*d, form[k2]);
         *d = v;
-        if (!kDeferReinitOut) out_el(kl->a.b.target, 2 * e + j, v);
+        out_el(kl->a.b.target, 2 * e + j, v);
     } else {
         const int jb = k2 - (5 * A + 2);
         const int j = 2 * jb;
@@ -409,41 +398,14 @@ __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, con
         const int64_t g = e * O * 2 + 2 * j;
         o[0] = blend_in(o[0], v[0]);
         o[1] = blend_in(o[1], v[1]);
-        if (!kDeferReinitOut) {
-            out_el(gob, g, o[0]);
-            out_el(gob, g + 1, o[1]);
-        }
+        out_el(gob, g, o[0]);
+        out_el(gob, g + 1, o[1]);
         if (j + 1 < O) {
             o[2] = blend_in(o[2], v[2]);
             o[3] = blend_in(o[3], v[3]);
-            if (!kDeferReinitOut) {
-                out_el(gob, g + 2, o[2]);
-                out_el(gob, g + 3, o[3]);
-            }
+            out_el(gob, g + 2, o[2]);
+            out_el(gob, g + 3, o[3]);
         }
-    }
-}
-
-// The re-initialised envs' obstacles and targets, from LDS to the global
-// state (kDeferReinitOut: issued after the re-init pass and its barrier, by
-// the block's nt threads). Inside the pass these stores queue behind the
-// other blocks' row stores in the CU's vector-memory path and hold the
-// pass's wave at issue.
-template <int A, int O, class Envs, class List>
-__device__ __forceinline__ void store_reinit_out(KArgsK *kl, const Envs &ev, const List &list,
-                                                 int nfin, int tid, int nt)
-{
-    float *gob = kl->a.b.obstacles;
-    float *gtg = kl->a.b.target;
-    constexpr int NV = 2 * O + 2;
-    for (int i = tid; i < nfin * NV; i += nt) {
-        const int fe = i / NV, k = i - fe * NV;
-        const int c = list[fe];
-        const int64_t e = ev.env(c);
-        if (k < 2 * O)
-            out_el(gob, e * O * 2 + k, ev.obst(c)[k]);
-        else
-            out_el(gtg, 2 * e + (k - 2 * O), ev.targ(c)[k - 2 * O]);
     }
 }
 
@@ -500,7 +462,7 @@ __device__ __forceinline__ void reinit_reobs_tpl(KArgsK *kl, const Envs &ev, con
             float *d = tg ? ev.targ(c) + (k2 - 5 * A) : ev.state(c) + k2;
             const float vb = blend_in(*d, form[k2]);
             *d = vb;
-            if (tg && !kDeferReinitOut) out_el(gtg, 2 * e + (k2 - 5 * A), vb);
+            if (tg) out_el(gtg, 2 * e + (k2 - 5 * A), vb);
             if ((tg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(form[k2]))
                 *unclean = 1;
         }
@@ -540,25 +502,11 @@ __device__ __forceinline__ void reinit_reobs_tpl(KArgsK *kl, const Envs &ev, con
             float *ow = ev.obst(c) + 2 * j;
             ow[0] = px;
             ow[1] = py;
-            if (!kDeferReinitOut) {
-                out_el(gob, e * O * 2 + 2 * j, px);
-                out_el(gob, e * O * 2 + 2 * j + 1, py);
-            }
+            out_el(gob, e * O * 2 + 2 * j, px);
+            out_el(gob, e * O * 2 + 2 * j + 1, py);
         }
     }
 }
-
-// A wave-uniform ballot mask as a list: entry fe is the env code of the
-// fe-th set bit (scalar bit clears; fe is wave-uniform)
-struct BitList {
-    uint64_t fm;
-    __device__ int operator[](int fe) const
-    {
-        uint64_t m = fm;
-        for (int i = 0; i < fe; ++i) m &= m - 1ull;
-        return (int)__builtin_ctzll(m);
-    }
-};
 
 // The finished envs of a block as a wave-uniform ballot mask (env code = bit
 // position; the env-block kernel): entry fe is the fe-th set bit, found by

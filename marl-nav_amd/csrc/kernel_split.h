@@ -110,18 +110,6 @@ constexpr bool kSplitTplPass = kSplitTpl<A, O> && (64 * kWavesPerBlock) % O == 0
 // and the per-env phase (the A3 env-block kernel's overlap): each wave parks
 // its envs' collision bits with their step numbers and `terminates` flags, so
 // the other waves find the finished set without waiting for wave 0
-// ... and each wave finishing its own envs' row rewards and per-env phase
-// right after its observe phase (no wait for the workgroup's slowest wave,
-// no serial pass on wave 0), storing its tile at once when none of its envs
-// finished; the workgroup's finished envs then go through the one-pass
-// re-init after one barrier, and only their waves store after it
-template <int A, int O>
-constexpr bool kSplitOwnEnv = kSplitTplPass<A, O> && !kSplitRRLeader<A, O> && MARLNAV_SPLIT_OWN_ENV;
-
-template <int A, int O>
-constexpr bool kSplitOverlap = kSplitTplPass<A, O> && !kSplitRRLeader<A, O> &&
-                               (64 * (kWavesPerBlock - 1)) % O == 0 && MARLNAV_SPLIT_OVERLAP;
-
 // Extra LDS cycles of the workgroup-spread row-reward read (kernel_split.h,
 // wave 0, lane = tile cw * R + row rw, reading the row's K bond terms at
 // tile base cw * F + BOND, row stride K, one ds_read_b32 per term): banks are
@@ -193,11 +181,10 @@ struct SplitPlan {
     // after the waves' regions: finished-env counts and slots of the
     // workgroup, the `unclean` word (reinit_block), then (kSplitTpl) the
     // formation and template at FTP
-    // (+ kWavesPerBlock * EPW step numbers and as many `terminates` flags and
-    // collision bits: the workgroup's per-env inputs, parked for wave 0's
-    // per-env phase and (kSplitOverlap) the other waves' finished set)
+    // (+ kWavesPerBlock * EPW step numbers and as many `terminates` flags:
+    // the workgroup's per-env inputs, parked for wave 0's per-env phase)
     static constexpr int ENVIN = (kWavesPerBlock * (1 + EPW) + 1 + 3) & ~3;
-    static constexpr int FTP = (ENVIN + 3 * kWavesPerBlock * EPW + 3) & ~3;
+    static constexpr int FTP = (ENVIN + 2 * kWavesPerBlock * EPW + 3) & ~3;
     // then (kSplitSpread shapes with O <= 8, native re-init) the fresh
     // obstacle draws of the workgroup's EW envs, component k of obstacle j of
     // env code c at PRE + (2j + k) * EW + c (kernel_reinit.h native_obst_draws)
@@ -576,7 +563,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     const float *tge = wl + SP::TG + 2 * el;
     float *orow = wl + SP::OBS + rowc * SP::DP;
     float *brow = wl + SP::BOND + rowc * (A - 1);
-    uint64_t colm = 0ull;  // row leaders of rows that collided (kSplitOverlap)
     {
         // wave-uniform choice of the pair math (coord_ok);
         // worth its check only when each lane evaluates many pairs
@@ -604,7 +590,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         if (!OBS_ONLY) {
             const unsigned fl = lpr_or<LPR>(t.fl);
             const int band = lpr_sum<LPR>(t.band);
-            if constexpr (kSplitOverlap<A, O>) colm = __ballot(row_on && q == 0 && (fl & 10u));
             wave_sync();  // bond terms of the row are in LDS
             if (row_on && q == 0) {
                 if constexpr (kSplitTgtInAg<A, O, LPR> || kSplitTgtInOb<A, O, LPR>) {
@@ -625,9 +610,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     }
     STAMP(3);
 
-    // ---- the tile's rows and states from LDS to global memory (at the
-    // end of the step, or - kSplitOwnEnv - as soon as none of the wave's
-    // envs finished)
+    // ---- the tile's rows and states from LDS to global memory (the end of
+    // the step)
     const auto store_tile = [&]() {
         {
             const float *src = wl + SP::OBS;
@@ -726,7 +710,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             }
         }
     };
-    bool own_done = false;  // this wave's tile already stored (kSplitOwnEnv)
 
     if (!OBS_ONLY) {
         wave_sync();
@@ -734,14 +717,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         // reward rows `red` (A float4: r_miss, r_hit, flags), step number and
         // `terminates` in); returns fin and sets the counter flags
         bool tr_l = false, co_l = false, ta_l = false;
-        // workgroup-spread shapes: wave 0's five per-env stores wait until
-        // after the per-env barrier (kSplitDeferEnvOut), so that they do not
-        // hold wave 0 - and the workgroup at that barrier - at issue behind
-        // the other workgroups' tile stores in the CU's vector-memory path
-        constexpr bool kDeferEnv = kSplitSpread<A, O> && MARLNAV_SPLIT_DEFER_ENV_OUT;
-        float dv_rew = 0.0f, dv_sn = 0.0f;
-        unsigned dv_fl = 0u;
-        bool dv_on = false;
         const auto per_env = [&](int64_t e, const float4 *red, float sn_v, unsigned term_v,
                                  float *s5, float *obl, float *tgl) -> bool {
             unsigned any_col = 0u, all_in = 1u;
@@ -759,18 +734,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 #pragma unroll
             for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
             const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
-            dv_rew = rsum / (float)A;                          // torch.mean (:233)
-            if (!kDeferEnv) out_el(b.reward, e, dv_rew);
+            out_el(b.reward, e, rsum / (float)A);             // torch.mean (:233)
             float step_num = sn_v + 1.0f;                      // :96
             const bool truncated = step_num > pr.trunc_after;  // :97
             const bool term_old = term_v != 0u;
             const bool terminated = any_col || term_old;       // :213-214
-            dv_fl = (!term_old && all_in ? 1u : 0u) | (terminated ? 2u : 0u) | (truncated ? 4u : 0u);
-            if (!kDeferEnv) {
-                out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
-                out_el(b.terminated, e, (uint8_t)terminated);
-                out_el(b.truncated, e, (uint8_t)truncated);
-            }
+            out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
+            out_el(b.terminated, e, (uint8_t)terminated);
+            out_el(b.truncated, e, (uint8_t)truncated);
             const bool fin = truncated || terminated;          // :102-104
             if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
                 KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -805,9 +776,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 out_el(gtg, 2 * e + 1, tgl[1]);
             }
             if (fin) step_num = blend_in(step_num, 0.0f);
-            dv_sn = step_num;
-            dv_on = true;
-            if (!kDeferEnv) out_el(b.step_num, e, step_num);
+            out_el(b.step_num, e, step_num);
             tr_l = truncated;
             co_l = any_col;
             ta_l = all_in;
@@ -827,9 +796,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             int *unclean = bslot + kWavesPerBlock * EPW;
             float *bsn = reinterpret_cast<float *>(bcnt) + SP::ENVIN;
             unsigned *bterm = reinterpret_cast<unsigned *>(bsn + kWavesPerBlock * EPW);
-            unsigned *bcol = bterm + kWavesPerBlock * EPW;
-            // waves 1..3 re-initialise under wave 0's per-env phase
-            const bool ovl = kSplitOverlap<A, O> && !NOISY && tpl_on && live == kWavesPerBlock;
             if (threadIdx.x == 0) *unclean = 0;
             if (tpl_on) {  // (uniform: every wave holds its part)
                 float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
@@ -839,72 +805,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     if (idx < SP::NCP) ftp[idx] = cp[k2];
                 }
             }
-            // kSplitOwnEnv (full workgroups with the formation template)
-            const bool own = kSplitOwnEnv<A, O> && !NOISY && tpl_on && live == kWavesPerBlock;
-            if (own) {
-                if ((int)lane < nr) {  // this wave's rows: their reward terms
-                    float4 *rp = reinterpret_cast<float4 *>(wl + SP::RED) + lane;
-                    const float4 tv = *rp;
-                    *rp = row_reward(tv.x, tv.y, __float_as_uint(tv.z), __float_as_int(tv.w),
-                                     wl + SP::BOND + (int)lane * (A - 1));
-                }
-                wave_sync();
-                bool fin = false;
-                if (env_on)
-                    fin = per_env(e0 + lane, reinterpret_cast<const float4 *>(wl + SP::RED) + A * lane,
-                                  sn_in, term_in, st + 5 * A * lane, wl + SP::OB + 2 * O * lane,
-                                  wl + SP::TG + 2 * lane);
-                const uint64_t fm = __ballot(fin);
-                if (fin)  // SplitFinList: env codes wib * EPW + env
-                    bslot[wib * EPW + (int)__builtin_amdgcn_mbcnt_hi(
-                                          (unsigned)(fm >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] =
-                        wib * EPW + (int)lane;
-                if (lane == 0) bcnt[wib] = (int)__popcll(fm);
-                c_trunc = __popcll(__ballot(tr_l));
-                c_col = __popcll(__ballot(co_l));
-                c_tar = __popcll(__ballot(ta_l));
-                if (fm == 0ull && !(MARLNAV_AB & 2)) {
-                    store_tile();
-                    own_done = true;
-                }
-            }
             if (env_on) {
                 bsn[wib * EPW + (int)lane] = sn_in;
                 bterm[wib * EPW + (int)lane] = term_in;
-                if constexpr (kSplitOverlap<A, O>) {
-                    // this env's rows: lanes [lane, lane + 1) * A * LPR
-                    constexpr int LE = A * LPR;
-                    const uint64_t emask = LE == 64 ? ~0ull : ((1ull << (LE % 64)) - 1ull);
-                    bcol[wib * EPW + (int)lane] = ((colm >> (((int)lane * LE) % 64)) & emask) != 0ull;
-                }
             }
             __syncthreads();
             STAMP(4);
             if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
-            if constexpr (kSplitOwnEnv<A, O>) {
-                if (own) {
-                    const SplitFinList<EPW> olist = SplitFinList<EPW>::make(bcnt, bslot, live);
-                    if (const int nfin = (MARLNAV_AB & 1) ? 0 : olist.total()) {
-                        KArgsK *kl = kargs_late<kHotKargsOff>();
-                        const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP>
-                            ev{lds, blk0 * EPW};
-                        const float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
-                        const int tid = (int)threadIdx.x, nt = 64 * kWavesPerBlock;
-                        reinit_reobs_tpl<A, O, 64 * kWavesPerBlock>(
-                            kl, ev, ftp, reinterpret_cast<const float2 *>(ftp + SP::NF), olist,
-                            nfin, pr.cap_distance, tid, unclean);
-                        __syncthreads();
-                        if (*unclean) {  // an agent or target off the formation: every pair
-                            reobs_block<A, O>(ev, olist, nfin, pr.cap_distance, tid, nt);
-                            __syncthreads();
-                        }
-                    }
-                }
-            }
-            if (!own) {  // ---- wave 0's per-env phase for the whole workgroup
             if (wib == 0) {
-                if (MARLNAV_SPLIT_ENV_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_SPLIT_ENV_PRIO);
                 // every row of the workgroup: its reward terms (one lane per
                 // row, all 64 lanes busy where the row leaders were 1 in LPR)
                 static_assert(kWavesPerBlock * R <= 64, "one lane per row of the workgroup");
@@ -939,39 +847,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 c_col = __popcll(__ballot(co_l));
                 c_tar = __popcll(__ballot(ta_l));
                 STAMPX(1);
-                if (MARLNAV_SPLIT_ENV_PRIO) __builtin_amdgcn_s_setprio(0);
-            } else if constexpr (kSplitOverlap<A, O>) {
-                if (ovl) {
-                    // the finished set from the parked inputs (the same tests
-                    // as per_env: :96-97, :102-104, :213-214), then the
-                    // one-pass re-init and re-observation on 64 * 3 threads
-                    const int ce = (int)lane;
-                    const bool on = ce < live * EPW && blk0 * EPW + ce < P;
-                    const bool fin = on && (bsn[ce] + 1.0f > pr.trunc_after || bterm[ce] != 0u ||
-                                            bcol[ce] != 0u);
-                    const uint64_t fm = __ballot(fin);
-                    if (fm && !(MARLNAV_AB & 1)) {  // (AB 1: timing only)
-                        KArgsK *kl = kargs_late<kHotKargsOff>();
-                        const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP>
-                            ev{lds, blk0 * EPW};
-                        const float *ftp = lds + kWavesPerBlock * SP::FLOATS + SP::FTP;
-                        reinit_reobs_tpl<A, O, 64 * (kWavesPerBlock - 1)>(
-                            kl, ev, ftp, reinterpret_cast<const float2 *>(ftp + SP::NF),
-                            BitList{fm}, (int)__popcll(fm), pr.cap_distance,
-                            (int)threadIdx.x - 64, unclean);
-                    }
-                }
             }
             __syncthreads();
             STAMPX(2);
-            if (kDeferEnv && wib == 0 && dv_on) {  // wave 0's per-env outputs (above)
-                const int64_t e = blk0 * EPW + (int)lane;
-                out_el(b.reward, e, dv_rew);
-                out_el(b.terminates, e, (uint8_t)(dv_fl & 1u));
-                out_el(b.terminated, e, (uint8_t)((dv_fl >> 1) & 1u));
-                out_el(b.truncated, e, (uint8_t)((dv_fl >> 2) & 1u));
-                out_el(b.step_num, e, dv_sn);
-            }
             if (MARLNAV_AB & 32768) return;  // (AB 32768: timing only - per-env done, then exit)
             const FlatFinList list{bslot, bcnt[0]};
 #if MARLNAV_STAMPS
@@ -985,17 +863,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 const int tid = (int)threadIdx.x, nt = 64 * live;
                 // fused native re-init + re-observation recomputes a Philox
                 // block per obstacle pair: only for few obstacles
-                if (ovl) {  // the pass ran above
-                    if (kDeferReinitOut) store_reinit_out<A, O>(kl, ev, list, nfin, tid, nt);
-                    if (*unclean) {  // an agent or target off the formation: every pair
-                        reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
-                        __syncthreads();
-                    }
-                } else if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
+                if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
                     reinit_reobs_native<A, O, SP::EW>(kl, ev, kl->a.b.formation, list, nfin,
                                                       pr.cap_distance, tid, nt, pre);
                     __syncthreads();
-                    if (kDeferReinitOut) store_reinit_out<A, O>(kl, ev, list, nfin, tid, nt);
                 } else if (kSplitTplPass<A, O> && tpl_on && live == kWavesPerBlock) {
                     if constexpr (kSplitTplPass<A, O>) {
                         // one pass (formation and template parked by every wave)
@@ -1005,7 +876,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                             nfin, pr.cap_distance, tid, unclean);
                         __syncthreads();
                         STAMPX(3);
-                        if (kDeferReinitOut) store_reinit_out<A, O>(kl, ev, list, nfin, tid, nt);
                         if (*unclean) {  // an agent or target off the formation: every pair
                             reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, nt);
                             __syncthreads();
@@ -1021,7 +891,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                     __syncthreads();
                 }
             }
-            }  // (!own)
         } else {
             bool fin = false;
             if (env_on)
@@ -1062,7 +931,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     // ---- stream the tile out (obs rows and states from LDS)
     wave_sync();
     if (MARLNAV_AB & 2) return;  // (AB 2: timing only - no store)
-    if (!own_done) store_tile();
+    store_tile();
     STAMP(6);
     if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
         KArgsK *kl = kargs_late<kHotKargsOff>();

@@ -50,15 +50,6 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_AB_NOREFC
 #define MARLNAV_AB_NOREFC 0
 #endif
-// Split kernel, workgroup-spread many-obstacle shapes: the one-pass re-init
-// on waves 1..3 under wave 0's per-env phase (1, A/B builds) or after it (0).
-// Measured slower at 4096x16x32 (graph replay 11.81 -> 12.31 us, rocprof
-// 12.74 -> 13.40 us over 200 steps from a fresh env) although the stamps
-// build shows the workgroups with finished envs 0.7 us shorter: their tail
-// then competes with the other workgroups' observe phase for the SIMDs.
-#ifndef MARLNAV_SPLIT_OVERLAP
-#define MARLNAV_SPLIT_OVERLAP 0
-#endif
 // Env-block kernel: wave 0's per-env phase (the block's latency chain while
 // its other waves wait at the barrier) at this s_setprio over the other
 // blocks' waves on its SIMD. A/B (profiles/r04_ab_env_prio.txt, graph
@@ -67,32 +58,8 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_ENV_PRIO
 #define MARLNAV_ENV_PRIO 3
 #endif
-// A/B builds: the split kernel's wave-0 per-env phase / the env-block
-// kernel's re-init pass (waves 1..A-1 of blocks with finished envs) at this
-// s_setprio
-#ifndef MARLNAV_SPLIT_ENV_PRIO
-#define MARLNAV_SPLIT_ENV_PRIO 0
-#endif
-#ifndef MARLNAV_TAIL_PRIO
-#define MARLNAV_TAIL_PRIO 0
-#endif
-// Env-block kernel: early_out (A/B builds, kernel_block.h)
-#ifndef MARLNAV_EARLY_OUT
-#define MARLNAV_EARLY_OUT 0
-#endif
-// Split kernel, workgroup-spread shapes: wave 0's per-env stores after the
-// per-env barrier (1, A/B builds: no change at 4096x16x32, 11.96 vs 11.97 us)
-// or inside the per-env phase (0)
-#ifndef MARLNAV_SPLIT_DEFER_ENV_OUT
-#define MARLNAV_SPLIT_DEFER_ENV_OUT 0
-#endif
-// Env-block kernel: wave 0's per-env stores and counter atomics after the
-// per-env barrier (A/B builds)
-#ifndef MARLNAV_DEFER_BLOCK_ENV_OUT
-#define MARLNAV_DEFER_BLOCK_ENV_OUT 0
-#endif
-// Split kernel, kSplitTplPass shapes: each wave's own row rewards and
-// per-env phase before the workgroup barrier (kSplitOwnEnv)
-#ifndef MARLNAV_SPLIT_OWN_ENV
-#define MARLNAV_SPLIT_OWN_ENV 0
-#endif
+// Round-4 A/B variants measured and removed from the sources (in git history
+// at bc24ae1, DESIGN.md §5 "Round 4"): MARLNAV_EARLY_OUT,
+// MARLNAV_DEFER_BLOCK_ENV_OUT, MARLNAV_TAIL_PRIO (env-block kernel);
+// MARLNAV_SPLIT_OVERLAP, MARLNAV_SPLIT_OWN_ENV, MARLNAV_SPLIT_DEFER_ENV_OUT,
+// MARLNAV_SPLIT_ENV_PRIO (split kernel); MARLNAV_DEFER_REINIT_OUT (re-init).
