@@ -33,7 +33,10 @@ __global__ void __launch_bounds__(192) store_barrier_kernel(float *out, int iter
     if (MODE == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     float acc = (float)tid;
     if (w == 0)
-        for (int i = 0; i < iters; ++i) acc = __builtin_fmaf(acc, 1.0001f, 0.5f);
+        for (int i = 0; i < iters; i += 16) {  // (16 per trip: the chain, not the loop branch)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc = __builtin_fmaf(acc, 1.0001f, 0.5f);
+        }
     __syncthreads();
     if (MODE == 2) stores();
     if (acc == 12345.0f) sink[0] = acc;
