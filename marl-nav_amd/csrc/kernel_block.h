@@ -139,6 +139,18 @@ __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float
         if ((k + 1) * NT <= Q2 || tid + k * NT < Q2) out_st4<kNtRows>(d2 + 4 * (tid + k * NT), v2[k]);
 }
 
+// Where a block with no finished env stores its rows and states: under the
+// per-env phase, from waves 1..A-1 (true), or after the last barrier. The
+// stores hold their waves at issue until the HBM-bound write burst drains
+// (DESIGN.md §5 "Where the stores go"): that pays where the observe phase is
+// long against the burst and loses at A3/O3 (graph replay, early vs after,
+// profiles/r04_ab_early_out.txt: 65536x3x8 10.54 -> 9.81 us, 131072x3x8
+// 18.10 -> 17.44, 32768x3x8 8.19 -> 8.07; 65536x3x3 6.98 -> 7.13, 16384x3x3
+// 5.18 -> 5.29, 131072x3x3 11.43 -> 11.53). MARLNAV_EARLY_OUT 0 / 1 forces it
+// (A/B builds).
+template <int A, int O>
+constexpr bool kBlockEarlyOut = MARLNAV_EARLY_OUT < 0 ? O >= 8 : MARLNAV_EARLY_OUT != 0;
+
 // Phases (one block barrier after each of the first four): stage | move +
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
@@ -374,6 +386,11 @@ __global__ void __launch_bounds__(64 * A)
     float *gobs = in_sgpr(b.obs + e0 * (A * D));
     if (OBS_ONLY) block_store(gobs, obs_rows, nrow * D, tid, NT, wt);
     const bool norm = !OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM);
+    // kBlockEarlyOut: a block with no finished env streams its rows and
+    // states from waves 1..A-1 under wave 0's per-env phase (they have
+    // nothing else to do there; blocks with finished envs keep the stores
+    // after their re-init). early: this block's stores left early.
+    bool early = false;
     if (!OBS_ONLY) {
         int *list = reinterpret_cast<int *>(lds + BP::LIST);
         int *flg = reinterpret_cast<int *>(lds + BP::FLG);
@@ -445,6 +462,7 @@ __global__ void __launch_bounds__(64 * A)
             }
             STAMPX(1);  // (wave 0: the per-env outputs issued)
             const uint64_t finmask = __ballot(fin);
+            early = kBlockEarlyOut<A, O> && overlap && full && !norm && finmask == 0ull;
             if (fin)
                 list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
                                                __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] = l;
@@ -482,6 +500,10 @@ __global__ void __launch_bounds__(64 * A)
                       reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
             }
             const uint64_t fm = __ballot(fin);
+            early = kBlockEarlyOut<A, O> && full && !norm && fm == 0ull;
+            if (early && !(MARLNAV_AB & 2))
+                block_store2<E * A * D, E * A * 5, NT - 64>(
+                    gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)), st, tid - 64, wt);
             STAMPX(0);
             if (fm && !(MARLNAV_AB & 1)) {
                 STAMPX(1);
@@ -508,7 +530,7 @@ __global__ void __launch_bounds__(64 * A)
     }
     STAMP(5);
     if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
-        if (!(MARLNAV_AB & 2))
+        if (!(MARLNAV_AB & 2) && !early)
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)),
                                                st, tid, wt);  // (E = 64: whole 16-byte pieces)
     } else if (!OBS_ONLY && full && NT % D == 0) {

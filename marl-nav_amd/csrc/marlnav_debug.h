@@ -59,7 +59,13 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #define MARLNAV_ENV_PRIO 3
 #endif
 // Round-4 A/B variants measured and removed from the sources (in git history
-// at bc24ae1, DESIGN.md §5 "Round 4"): MARLNAV_EARLY_OUT,
+// at bc24ae1, DESIGN.md §5 "Round 4"): MARLNAV_EARLY_OUT's first forms,
 // MARLNAV_DEFER_BLOCK_ENV_OUT, MARLNAV_TAIL_PRIO (env-block kernel);
 // MARLNAV_SPLIT_OVERLAP, MARLNAV_SPLIT_OWN_ENV, MARLNAV_SPLIT_DEFER_ENV_OUT,
 // MARLNAV_SPLIT_ENV_PRIO (split kernel); MARLNAV_DEFER_REINIT_OUT (re-init).
+// Env-block kernel: blocks with no finished env stream their rows from waves
+// 1..A-1 under the per-env phase (1), after it (0), or by shape (-1: the
+// product's choice, kBlockEarlyOut in kernel_block.h)
+#ifndef MARLNAV_EARLY_OUT
+#define MARLNAV_EARLY_OUT -1
+#endif
