@@ -139,6 +139,41 @@ __device__ __forceinline__ void block_store2(float *__restrict__ d1, const float
         if ((k + 1) * NT <= Q2 || tid + k * NT < Q2) out_st4<kNtRows>(d2 + 4 * (tid + k * NT), v2[k]);
 }
 
+// The end-of-step state of one env (environment.py:96-97 step count and
+// truncation, :213-219 collision / target flags, :102-104 finished) from its
+// agents' row flags (RowOut.flags: bit0 collision, bit1 in target) and its
+// staged step_num / terminates. The one definition of "finished": wave 0's
+// per-env phase (its outputs) and waves 1..A-1 (the re-init set and the
+// early-store decision) both evaluate it on the same LDS inputs, so the two
+// finished sets cannot drift apart.
+struct EnvEnd {
+    unsigned any_col, all_in;
+    float step_num;  // incremented (:96)
+    bool truncated, term_old, terminated, fin;
+};
+
+// flag(i): agent i's RowOut.flags word
+template <int A, class F>
+__device__ __forceinline__ EnvEnd env_end(F flag, float step_num_old, uint8_t terminates_old,
+                                          float trunc_after)
+{
+    EnvEnd e;
+    e.any_col = 0u;
+    e.all_in = 1u;
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+        const unsigned f = flag(i);
+        e.any_col |= f & 1u;
+        e.all_in &= (f >> 1) & 1u;
+    }
+    e.step_num = step_num_old + 1.0f;             // :96
+    e.truncated = e.step_num > trunc_after;       // :97
+    e.term_old = terminates_old != 0;
+    e.terminated = e.any_col != 0u || e.term_old;  // :213-214
+    e.fin = e.truncated || e.terminated;          // :102-104
+    return e;
+}
+
 // Where a block with no finished env stores its rows and states: under the
 // per-env phase, from waves 1..A-1 (true), or after the last barrier. The
 // stores hold their waves at issue until the HBM-bound write burst drains
@@ -402,34 +437,36 @@ __global__ void __launch_bounds__(64 * A)
             bool fin = false, tr_l = false, co_l = false, ta_l = false;
             if (env_on) {
                 const int64_t e = e0 + l;
-                float4 rr[A];
-#pragma unroll
-                for (int i = 0; i < A; ++i) rr[i] = red[A * l + i];
-                unsigned any_col = 0u, all_in = 1u;
+                float rx[A], ry[A];
+                unsigned rf[A];
 #pragma unroll
                 for (int i = 0; i < A; ++i) {
-                    const unsigned f = __float_as_uint(rr[i].z);
-                    any_col |= f & 1u;
-                    all_in &= (f >> 1) & 1u;
+                    const float4 t = red[A * l + i];
+                    rx[i] = t.x;
+                    ry[i] = t.y;
+                    rf[i] = __float_as_uint(t.z);
                 }
+                const EnvEnd ee = env_end<A>([&](int i) { return rf[i]; }, lds[BP::SN + l],
+                                             reinterpret_cast<const uint8_t *>(lds + BP::TM)[l],
+                                             pr.trunc_after);
+                const unsigned any_col = ee.any_col, all_in = ee.all_in;
                 float rv[A];
 #pragma unroll
-                for (int i = 0; i < A; ++i) rv[i] = all_in ? rr[i].y : rr[i].x;
+                for (int i = 0; i < A; ++i) rv[i] = all_in ? ry[i] : rx[i];
                 STAMPX(0);  // (wave 0: the reward terms read)
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
                 if (!(MARLNAV_AB & 1024))  // (AB 1024: timing only, no per-env stores)
                 out_el(b.reward, e, rsum / (float)A);              // torch.mean (:233)
 
-                float step_num = lds[BP::SN + l] + 1.0f;           // :96
-                const bool truncated = step_num > pr.trunc_after;  // :97
-                const bool term_old = reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
-                const bool terminated = any_col || term_old;       // :213-214
+                const float step_num = ee.step_num;
+                const bool truncated = ee.truncated, term_old = ee.term_old;
+                const bool terminated = ee.terminated;
                 if (!(MARLNAV_AB & 1024)) {
                 out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
                 out_el(b.terminated, e, (uint8_t)terminated);
                 out_el(b.truncated, e, (uint8_t)truncated);
                 }
-                fin = truncated || terminated;                     // :102-104
+                fin = ee.fin;
                 if (NOISY && fin) {  // noisy native re-init: serial per env
                     KArgsK *kl = kargs_late<kHotKargsOff>();
                     {
@@ -492,12 +529,11 @@ __global__ void __launch_bounds__(64 * A)
             // (:105) of those envs. Disjoint LDS: wave 0 reads red/SN/TM; this
             // writes the states, obstacles, target and rows of finished envs.
             bool fin = false;
-            if (l < ne) {
-                unsigned any_col = 0u;
-#pragma unroll
-                for (int i = 0; i < A; ++i) any_col |= __float_as_uint(red[A * l + i].z) & 1u;
-                fin = lds[BP::SN + l] + 1.0f > pr.trunc_after || any_col != 0u ||
-                      reinterpret_cast<const uint8_t *>(lds + BP::TM)[l] != 0;
+            if (l < ne) {  // (the same env_end as wave 0's, on the same LDS inputs)
+                fin = env_end<A>([&](int i) { return __float_as_uint(red[A * l + i].z); },
+                                 lds[BP::SN + l],
+                                 reinterpret_cast<const uint8_t *>(lds + BP::TM)[l], pr.trunc_after)
+                          .fin;
             }
             const uint64_t fm = __ballot(fin);
             early = kBlockEarlyOut<A, O> && full && !norm && fm == 0ull;

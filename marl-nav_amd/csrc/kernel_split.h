@@ -106,10 +106,6 @@ constexpr bool kSplitRRLeader = !kSplitSpread<A, O> || O <= 8 || MARLNAV_SPLIT_R
 template <int A, int O>
 constexpr bool kSplitTplPass = kSplitTpl<A, O> && (64 * kWavesPerBlock) % O == 0;
 
-// ... and that pass run by waves 1..3 while wave 0 finishes the rows' rewards
-// and the per-env phase (the A3 env-block kernel's overlap): each wave parks
-// its envs' collision bits with their step numbers and `terminates` flags, so
-// the other waves find the finished set without waiting for wave 0
 // Extra LDS cycles of the workgroup-spread row-reward read (kernel_split.h,
 // wave 0, lane = tile cw * R + row rw, reading the row's K bond terms at
 // tile base cw * F + BOND, row stride K, one ds_read_b32 per term): banks are

@@ -63,6 +63,8 @@ def load():
         lib.oracle_acos_device_range.restype = None
         lib.oracle_set_acos_mode.argtypes = [ctypes.c_int]
         lib.oracle_set_acos_mode.restype = None
+        lib.oracle_get_acos_mode.argtypes = []
+        lib.oracle_get_acos_mode.restype = ctypes.c_int
         lib.oracle_set_vsqrt_grid.argtypes = [P, ctypes.c_int64, P, ctypes.c_int64]
         lib.oracle_set_vsqrt_grid.restype = None
         # the measured v_sqrt_f32 offsets the kernels' acos sees
@@ -243,14 +245,21 @@ class acos_mode:
 
     def __init__(self, mode):
         self.mode = mode
+        self._saved = []
 
     def __enter__(self):
-        load().oracle_set_acos_mode(int(self.mode))
+        lib = load()
+        self._saved.append(int(lib.oracle_get_acos_mode()))  # nested uses restore in order
+        lib.oracle_set_acos_mode(int(self.mode))
         return self
 
     def __exit__(self, *exc):
-        load().oracle_set_acos_mode(ACOS_DEVICE)
+        load().oracle_set_acos_mode(self._saved.pop())
         return False
+
+
+def get_acos_mode():
+    return int(load().oracle_get_acos_mode())
 
 
 def acosf_range(first_bits, n):

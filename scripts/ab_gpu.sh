@@ -10,6 +10,7 @@ if [ "${TESTS:-1}" = 1 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_w.log 2>&1
 rc=$?; tail -2 gpurun_out/pytest_w.log; [ $rc -eq 0 ] || { grep -E 'FAIL|Error|assert' gpurun_out/pytest_w.log | head -20; exit $rc; }
 fi
-REPS=${REPS:-3} timeout -k 10 500 python scripts/ab_steady.py $CFGS marl-nav_amd/lib/libmarlnav.so $LIBS > gpurun_out/ab_w.txt 2>&1 || exit $?
+libs=""; for x in ${LIBS:-}; do case $x in */*) libs="$libs $x";; *) libs="$libs marl-nav_amd/lib/$x";; esac; done
+REPS=${REPS:-3} timeout -k 10 ${ABT:-500} python scripts/ab_steady.py $CFGS marl-nav_amd/lib/libmarlnav.so $libs > gpurun_out/ab_w.txt 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/ab_w.txt
 echo done

@@ -430,9 +430,13 @@ def test_oracle_device_acos_vs_reference(name, mk):
         args = (dm, pr, z["in_states"][k], z["in_obstacles"][k], z["in_target"][k],
                 z["in_step_num"][k], z["in_terminates"][k], z["actions"][k])
         fresh = (z["fresh_states"][k], z["fresh_obstacles"][k], z["fresh_target"][k])
-        o_glibc = orc.step(*args, fresh=fresh)
+        with orc.acos_mode(orc.ACOS_GLIBC):
+            o_glibc = orc.step(*args, fresh=fresh)
         with orc.acos_mode(orc.ACOS_DEVICE):
             o = orc.step(*args, fresh=fresh)
+        assert orc.get_acos_mode() == orc.ACOS_GLIBC  # (the autouse fixture's mode is back)
+        n_diff = int(np.count_nonzero(o["obs"].view(np.uint32) != o_glibc["obs"].view(np.uint32)))
+        assert n_diff > 0 or P * A < 4, "the two acos modes must be distinguishable here"
         where = f"{name} step {k}"
         for key in ("states", "reward", "terminated", "truncated"):
             np.testing.assert_array_equal(o[key], o_glibc[key], where + " " + key)
@@ -441,6 +445,18 @@ def test_oracle_device_acos_vs_reference(name, mk):
                          where=where)
         record_angle_stats("oracle F1 (device acos)", "reference", fields,
                            [z["obs_" + f][k] for f in OBS_FIELDS])
+
+
+def test_acos_mode_nests_and_restores():
+    """acos_mode restores the mode it found (not a fixed default), so a
+    nested use inside the autouse glibc fixture leaves glibc in force."""
+    assert orc.get_acos_mode() == orc.ACOS_GLIBC
+    with orc.acos_mode(orc.ACOS_DEVICE):
+        assert orc.get_acos_mode() == orc.ACOS_DEVICE
+        with orc.acos_mode(orc.ACOS_GLIBC):
+            assert orc.get_acos_mode() == orc.ACOS_GLIBC
+        assert orc.get_acos_mode() == orc.ACOS_DEVICE
+    assert orc.get_acos_mode() == orc.ACOS_GLIBC
 
 
 def test_acos_device_restatement_known_values():
