@@ -459,33 +459,74 @@ __device__ __forceinline__ void sincos_k(float th, float *s_out, float *c_out)
 }
 
 // ----------------------------------------------------------- native RNG
-__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
+// The native stream (rng='native'; a distributional match of the reference's
+// torch.rand draws, utils.py:381-398, checked by tests/test_native_rng_dist.py):
+// Philox2x32-10 (Salmon et al., SC'11: Random123's philox2x32 at its default
+// 10 rounds; its published known-answer vectors are checked in
+// tests/test_oracle_golden.py). Uniform #idx of env gid at step s is word
+// idx & 1 of block idx >> 1: counter (lo32(gid), lo32(s) ^ hi32(gid) *
+// 0x85EBCA77) under the key native_key(seed, idx >> 1, s), on torch.rand's
+// 24-bit grid. The key holds no per-env term, so where the block index is
+// wave-uniform (the env-block kernel's draws) it and its round increments
+// live in SGPRs. Obstacle j is block j (x = word 0, y = word 1): one block per
+// obstacle, so an A3/O3 env block draws exactly one block per thread
+// (Philox4x32-10, rounds 1-4, drew two 4-word blocks per env on two of the
+// three waves: 20 v_mad_u64_u32 per drawing lane against 10 here).
+// oracle/marlnav_oracle.c restates it.
+constexpr uint32_t kPhiloxM2 = 0xD256D193u, kPhiloxW = 0x9E3779B9u;
+
+__device__ __forceinline__ void philox2x32_10(uint32_t &c0, uint32_t &c1, uint32_t k)
 {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        // one v_mad_u64_u32 per product instead of v_mul_lo_u32 + v_mul_hi_u32
-        const uint64_t p0 = (uint64_t)c[0] * 0xD2511F53u, p1 = (uint64_t)c[2] * 0xCD9E8D57u;
-        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
-        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
-        c[0] = n0;
-        c[1] = lo1;
-        c[2] = n2;
-        c[3] = lo0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
+        // one v_mad_u64_u32 per round for the 64-bit product
+        const uint64_t p = (uint64_t)c0 * kPhiloxM2;
+        const uint32_t hi = (uint32_t)(p >> 32), lo = (uint32_t)p;
+        c0 = __builtin_amdgcn_bitop3_b32(hi, k, c1, 0x96);  // hi ^ k ^ c1 in one VALU
+        c1 = lo;
+        k += kPhiloxW;
     }
 }
 
-// uniform #idx of env gid at step s, in [0, 1) on a 24-bit grid
+// the 32-bit Philox key of block `blk` at step s: the 64-bit seed, the
+// block index and the high word of s (zero below 2^32 steps) folded by odd
+// multipliers (the counter carries the env id and the low word of s)
+__host__ __device__ constexpr uint32_t native_key(uint64_t seed, uint32_t blk, uint64_t s)
+{
+    return (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x9E3779B1u) ^
+           ((uint32_t)(s >> 32) * 0xC2B2AE3Du) ^ (blk * 0x27D4EB2Fu);
+}
+
+// block `blk` of env gid at step s: two 32-bit words
+__device__ __forceinline__ void native_block(uint64_t seed, uint32_t blk, uint64_t gid, uint64_t s,
+                                             uint32_t &r0, uint32_t &r1)
+{
+    r0 = (uint32_t)gid;
+    r1 = (uint32_t)s ^ ((uint32_t)(gid >> 32) * 0x85EBCA77u);
+    if (!(MARLNAV_AB & 4)) philox2x32_10(r0, r1, native_key(seed, blk, s));  // (AB 4: timing only)
+}
+
+// a 32-bit word -> [0, 1) on a 24-bit grid (torch.rand's fp32 values)
+__device__ __forceinline__ float native_u24(uint32_t r) { return (float)(r >> 8) * 0x1.0p-24f; }
+
+// uniform #idx of env gid at step s
 __device__ __forceinline__ float native_uniform(uint64_t seed, uint64_t gid, uint64_t s,
                                                 uint32_t idx)
 {
-    uint32_t c[4] = {idx >> 2, (uint32_t)s, (uint32_t)gid,
-                     (uint32_t)(gid >> 32) ^ ((uint32_t)(s >> 32) << 16)};
-    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const uint32_t r = c[idx & 3u];
-    return (float)(r >> 8) * 0x1.0p-24f;
+    uint32_t r0, r1;
+    native_block(seed, idx >> 1, gid, s, r0, r1);
+    return native_u24((idx & 1u) ? r1 : r0);
+}
+
+// obstacle j of env gid at step s, scaled like the reference's sampler
+// (utils.py:390-398): v[0] = x, v[1] = y
+__device__ __forceinline__ void native_obst_draw(uint64_t seed, uint64_t s, uint64_t gid, int j,
+                                                 float rx, float mx, float ry, float my, float v[2])
+{
+    uint32_t r0, r1;
+    native_block(seed, (uint32_t)j, gid, s, r0, r1);
+    v[0] = rx * (native_u24(r0) - 0.5f) + mx;
+    v[1] = ry * (native_u24(r1) - 0.5f) + my;
 }
 
 // _reinit_update (environment.py:86-90) for a finished env (mask 1):
@@ -503,16 +544,12 @@ __device__ void native_fresh_env(int A, int S, const MarlnavParams &pr,
                                  uint64_t sidx, float *st, float *ob, float *tg)
 {
     const auto put = [](float *d, float v) { *d = BLEND ? blend_in(*d, v) : v; };
-    for (int j = 0; j < S; j += 2) {  // one Philox block = 2 obstacles
-        uint32_t c[4] = {(uint32_t)(j >> 1), (uint32_t)sidx, (uint32_t)gid,
-                         (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16)};
-        philox4x32_10(c, (uint32_t)pr.seed, (uint32_t)(pr.seed >> 32));
-        put(ob + 2 * j, pr.obs_range_x * ((float)(c[0] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x);
-        put(ob + 2 * j + 1, pr.obs_range_y * ((float)(c[1] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y);
-        if (j + 1 < S) {
-            put(ob + 2 * j + 2, pr.obs_range_x * ((float)(c[2] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_x);
-            put(ob + 2 * j + 3, pr.obs_range_y * ((float)(c[3] >> 8) * 0x1.0p-24f - 0.5f) + pr.obs_mean_y);
-        }
+    for (int j = 0; j < S; ++j) {  // one Philox block per obstacle
+        float v[2];
+        native_obst_draw(pr.seed, sidx, gid, j, pr.obs_range_x, pr.obs_mean_x, pr.obs_range_y,
+                         pr.obs_mean_y, v);
+        put(ob + 2 * j, v[0]);
+        put(ob + 2 * j + 1, v[1]);
     }
     put(tg, formation[5 * A]);
     put(tg + 1, formation[5 * A + 1]);

@@ -274,30 +274,32 @@ __global__ void __launch_bounds__(64 * A)
     // native (non-noisy) re-init: waves 1..A-1 take the finished envs while
     // wave 0 runs the per-env phase (below)
     const bool overlap = !OBS_ONLY && !NOISY && !K->a.b.fresh_states;
-    // (one Philox block per thread at most: at A3/O8 the two passes cost the
-    // stage phase more than they save, 131072x3x8 18.4 -> 19.0 us)
-    constexpr bool kPre = E * ((O + 1) / 2) <= NT;
+    // (one Philox block per thread at most: O <= A. At A3/O8 the draws go
+    // to the finished-env tail instead: three blocks per thread here cost
+    // the stage phase more than they save there, 131072x3x8 18.4 -> 19.0 us
+    // with the round-4 Philox4x32)
+    constexpr bool kPre = E * O <= NT;
     if (kPre && overlap && !(MARLNAV_AB & 256)) {  // (AB 256: timing only, no draws)
         // the fresh obstacles of every env of the block (its Philox draws
         // depend only on seed, step and env id), drawn while the staging
         // loads are in flight: a finished env's re-init then reads them
         // instead of drawing after the per-env barrier, where the draws sat
-        // on the block's critical path (65536x3x3: 0.25 us of 0.63)
+        // on the block's critical path (65536x3x3: 0.25 us of 0.63). Item
+        // i = obstacle i / E of env i % E: at E = 64 the obstacle index is
+        // the wave's, so the Philox key is wave-uniform (SALU).
         KArgsK *kl = kargs_late<kHotKargsOff>();
         const uint64_t sidx = kl->a.step_idx, g0 = (uint64_t)(kl->a.env_offset + e0);
-        constexpr int NB = (O + 1) / 2;
         float *pre = lds + BP::FRESH;
 #pragma unroll
-        for (int k2 = 0; k2 * NT < E * NB; ++k2) {
+        for (int k2 = 0; k2 * NT < E * O; ++k2) {
             const int i = tid + k2 * NT;
-            const int l = i % E, jb = i / E;
-            if (((k2 + 1) * NT <= E * NB || i < E * NB) && l < ne) {
-                float v[4];
-                native_obst_draws(pr.seed, sidx, g0 + l, jb, pr.obs_range_x, pr.obs_mean_x,
-                                  pr.obs_range_y, pr.obs_mean_y, v);
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (2 * jb + k / 2 < O) pre[(4 * jb + k) * E + l] = v[k];
+            const int l = i % E, j = __builtin_amdgcn_readfirstlane(i / E);
+            if (((k2 + 1) * NT <= E * O || i < E * O) && l < ne) {
+                float v[2];
+                native_obst_draw(pr.seed, sidx, g0 + l, j, pr.obs_range_x, pr.obs_mean_x,
+                                 pr.obs_range_y, pr.obs_mean_y, v);
+                pre[(2 * j) * E + l] = v[0];
+                pre[(2 * j + 1) * E + l] = v[1];
             }
         }
     }
@@ -332,7 +334,10 @@ __global__ void __launch_bounds__(64 * A)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
     __syncthreads();
     STAMP(1);
-    if (MARLNAV_AB & 8192) return;  // (AB 8192: timing only - staged, then exit)
+    if (MARLNAV_AB & 8192) {  // (AB 8192: timing / census only - staged, then exit;
+        asm volatile("" ::"v"(sn), "v"(c), "v"(a1));  // the sin/cos kept alive)
+        return;
+    }
 
     // obstacle and target coordinates of the block for the pair-math choice
     // (below); read before the move writes LDS, so the reads overlap it

@@ -152,36 +152,15 @@ __device__ __forceinline__ void lds_row_write(float *dst, const float *row)
     }
 }
 
-__device__ __forceinline__ void philox_obst_block(uint32_t cc[4], int jb, uint64_t gid, uint64_t sidx,
-                                                  uint64_t seed)
-{
-    cc[0] = (uint32_t)jb;
-    cc[1] = (uint32_t)sidx;
-    cc[2] = (uint32_t)gid;
-    cc[3] = (uint32_t)(gid >> 32) ^ ((uint32_t)(sidx >> 32) << 16);
-    if (!(MARLNAV_AB & 4)) philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
-}
-
 // The block's fresh obstacle draws precomputed while its staging loads are in
-// flight (env-block kernel; the split kernel draws in the items): `pre` holds
-// component k (0 x, 1 y) of obstacle j of env code c at pre[(2j + k) * E + c].
-// The Philox block jb of env gid, as native_fresh_env draws it, scaled into
-// obstacle coordinates.
-__device__ __forceinline__ void native_obst_draws(uint64_t seed, uint64_t sidx, uint64_t gid, int jb,
-                                                  float rx, float mx, float ry, float my, float v[4])
-{
-    uint32_t cc[4];
-    philox_obst_block(cc, jb, gid, sidx, seed);
-    v[0] = rx * ((float)(cc[0] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-    v[1] = ry * ((float)(cc[1] >> 8) * 0x1.0p-24f - 0.5f) + my;
-    v[2] = rx * ((float)(cc[2] >> 8) * 0x1.0p-24f - 0.5f) + mx;
-    v[3] = ry * ((float)(cc[3] >> 8) * 0x1.0p-24f - 0.5f) + my;
-}
+// flight (env-block and few-obstacle split kernels): `pre` holds component k
+// (0 x, 1 y) of obstacle j of env code c at pre[(2j + k) * E + c]
+// (native_obst_draw, device_math.h).
 
 // Re-initialisation of the finished envs (environment.py:76-90, the sampler
 // call at :78) spread over the workgroup: one item per thread per pass - one
 // float of a fresh candidate (reference RNG) or of the formation template,
-// or one Philox block of two obstacles (native; the same draws as
+// or one obstacle's Philox block (native; the same draws as
 // native_fresh_env). Writes the LDS state and the global obstacles / target;
 // the agent rows go out with the final stores.
 // `unclean` (optional, native re-init): set to 1 when a finished env's
@@ -189,7 +168,7 @@ __device__ __forceinline__ void native_obst_draws(uint64_t seed, uint64_t sidx, 
 // non-finite old value blends to NaN), i.e. when the formation template
 // (reobs_block_tpl) does not describe the re-initialised env.
 // E > 0 (native re-init): the fresh obstacles come from `pre` (E envs,
-// native_obst_draws at stage time) instead of being drawn here.
+// native_obst_draw at stage time) instead of being drawn here.
 template <int A, int O, int E = 0, class Envs, class List>
 __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const float *form,
                                              const List &list, int nfin, int tid, int nt,
@@ -225,7 +204,7 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
         }
         return;
     }
-    constexpr int NB = (O + 1) / 2, NI = 5 * A + 2 + NB;
+    constexpr int NI = 5 * A + 2 + O;
     const uint64_t seed = kl->p.seed, sidx = kl->a.step_idx;
     const int64_t eoff = kl->a.env_offset;
     const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
@@ -248,14 +227,13 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
             out_el(gtg, 2 * e + j, v);
             if (unclean && __float_as_uint(v) != __float_as_uint(form[kk])) *unclean = 1;
         } else {
-            const int jb = kk - 5 * A - 2;  // obstacles 2jb, 2jb + 1
-            const int j = 2 * jb;
-            float v[4];
+            const int j = kk - 5 * A - 2;  // obstacle j
+            float v[2];
             if constexpr (E > 0) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) v[k] = (j + k / 2 < O) ? pre[(2 * j + k) * E + c] : 0.0f;
+                v[0] = pre[(2 * j) * E + c];
+                v[1] = pre[(2 * j + 1) * E + c];
             } else {
-                native_obst_draws(seed, sidx, (uint64_t)(eoff + e), jb, rx, mx, ry, my, v);
+                native_obst_draw(seed, sidx, (uint64_t)(eoff + e), j, rx, mx, ry, my, v);
             }
             float *o = ev.obst(c) + 2 * j;
             const int64_t g = e * O * 2 + 2 * j;
@@ -263,12 +241,6 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
             o[1] = blend_in(o[1], v[1]);
             out_el(gob, g, o[0]);
             out_el(gob, g + 1, o[1]);
-            if (j + 1 < O) {
-                o[2] = blend_in(o[2], v[2]);
-                o[3] = blend_in(o[3], v[3]);
-                out_el(gob, g + 2, o[2]);
-                out_el(gob, g + 3, o[3]);
-            }
         }
     }
 }
@@ -279,8 +251,8 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
 // native_fresh_env), so each observation item computes its own inputs
 // instead of waiting for a re-init pass and a barrier. Items per finished
 // env: A*(1+O+A-1) pairs (written into the packed rows), 5A+2 template
-// floats and ceil(O/2) Philox blocks (written to the LDS state and the
-// global obstacles/target).
+// floats and O Philox blocks, one per obstacle (written to the LDS state and
+// the global obstacles/target).
 //
 // With two or more waves the items go by kind: the first half of the waves
 // takes the pair items, the rest the template / obstacle items, so no wave
@@ -289,8 +261,8 @@ __device__ __forceinline__ void reinit_block(KArgsK *kl, const Envs &ev, const f
 // left skips the pass. `tid` and `nt` are wave-aligned.
 template <int A, int O>
 struct NativeItems {
-    static constexpr int NP = 1 + O + (A - 1), NB = (O + 1) / 2;
-    static constexpr int NPAIR = A * NP, NREST = 5 * A + 2 + NB;
+    static constexpr int NP = 1 + O + (A - 1);
+    static constexpr int NPAIR = A * NP, NREST = 5 * A + 2 + O;
 };
 
 
@@ -302,11 +274,12 @@ __device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, con
 {
     using IT = NativeItems<A, O>;
     const int ag = kk / IT::NP, p = kk - ag * IT::NP;
-    uint32_t cc[4] = {0u, 0u, 0u, 0u};
+    uint32_t ux = 0u, uy = 0u;
     const bool cargs = (MARLNAV_AB & 8) != 0;  // timing only: no kernel-argument loads
     if (!E && p >= 1 && p <= O)  // obstacle p - 1: its Philox block
-        philox_obst_block(cc, (p - 1) >> 1, (uint64_t)((cargs ? 0 : kl->a.env_offset) + ev.env(c)),
-                          cargs ? 7u : kl->a.step_idx, cargs ? 5u : kl->p.seed);
+        native_block(cargs ? 5u : kl->p.seed, (uint32_t)(p - 1),
+                     (uint64_t)((cargs ? 0 : kl->a.env_offset) + ev.env(c)),
+                     cargs ? 7u : kl->a.step_idx, ux, uy);
     // inputs: the blend of the env's current value (LDS; other items may be
     // blending it in place meanwhile - blend_in is idempotent) with its fresh
     // value (template or Philox draw)
@@ -327,12 +300,10 @@ __device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, con
             px = blend_in(oo[0], pre[(2 * (p - 1)) * E + c]);
             py = blend_in(oo[1], pre[(2 * (p - 1) + 1) * E + c]);
         } else {
-            const bool hi = ((p - 1) & 1) != 0;
-            const uint32_t ux = hi ? cc[2] : cc[0], uy = hi ? cc[3] : cc[1];
             const float rx = cargs ? 1000.f : kl->p.obs_range_x, mx = cargs ? 0.f : kl->p.obs_mean_x;
             const float ry = cargs ? 1000.f : kl->p.obs_range_y, my = cargs ? 0.f : kl->p.obs_mean_y;
-            px = blend_in(oo[0], rx * ((float)(ux >> 8) * 0x1.0p-24f - 0.5f) + mx);
-            py = blend_in(oo[1], ry * ((float)(uy >> 8) * 0x1.0p-24f - 0.5f) + my);
+            px = blend_in(oo[0], rx * (native_u24(ux) - 0.5f) + mx);
+            py = blend_in(oo[1], ry * (native_u24(uy) - 0.5f) + my);
         }
         sa = 1 + p;
         sd = 1 + O + p;
@@ -382,16 +353,15 @@ __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, con
         *d = v;
         out_el(kl->a.b.target, 2 * e + j, v);
     } else {
-        const int jb = k2 - (5 * A + 2);
-        const int j = 2 * jb;
-        float v[4];
+        const int j = k2 - (5 * A + 2);  // obstacle j
+        float v[2];
         if constexpr (E > 0) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = (j + k / 2 < O) ? pre[(2 * j + k) * E + c] : 0.0f;
+            v[0] = pre[(2 * j) * E + c];
+            v[1] = pre[(2 * j + 1) * E + c];
         } else {
-            native_obst_draws(kl->p.seed, kl->a.step_idx, (uint64_t)(kl->a.env_offset + e), jb,
-                              kl->p.obs_range_x, kl->p.obs_mean_x, kl->p.obs_range_y,
-                              kl->p.obs_mean_y, v);
+            native_obst_draw(kl->p.seed, kl->a.step_idx, (uint64_t)(kl->a.env_offset + e), j,
+                             kl->p.obs_range_x, kl->p.obs_mean_x, kl->p.obs_range_y,
+                             kl->p.obs_mean_y, v);
         }
         float *gob = kl->a.b.obstacles;
         float *o = ev.obst(c) + 2 * j;
@@ -400,12 +370,6 @@ __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, con
         o[1] = blend_in(o[1], v[1]);
         out_el(gob, g, o[0]);
         out_el(gob, g + 1, o[1]);
-        if (j + 1 < O) {
-            o[2] = blend_in(o[2], v[2]);
-            o[3] = blend_in(o[3], v[3]);
-            out_el(gob, g + 2, o[2]);
-            out_el(gob, g + 3, o[3]);
-        }
     }
 }
 
@@ -466,12 +430,12 @@ __device__ __forceinline__ void reinit_reobs_tpl(KArgsK *kl, const Envs &ev, con
             if ((tg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(form[k2]))
                 *unclean = 1;
         }
-        // obstacle j: its Philox block (obstacles 2jb, 2jb + 1) and blend
-        float v[4];
-        native_obst_draws(seed, sidx, (uint64_t)(eoff + e), j >> 1, rx, mx, ry, my, v);
+        // obstacle j: its Philox block and blend
+        float v[2];
+        native_obst_draw(seed, sidx, (uint64_t)(eoff + e), j, rx, mx, ry, my, v);
         const float *oo = ev.obst(c) + 2 * j;
-        const float px = blend_in(oo[0], (j & 1) ? v[2] : v[0]);
-        const float py = blend_in(oo[1], (j & 1) ? v[3] : v[1]);
+        const float px = blend_in(oo[0], v[0]);
+        const float py = blend_in(oo[1], v[1]);
         // its pairs with agents ag0, ag0 + agd, ... (per wave and agent: the
         // short sqrt / division sequences when every coordinate passes
         // coord_ok, IEEE otherwise)
@@ -536,7 +500,7 @@ __device__ __forceinline__ int list_code(const MaskList &l, int fe, int lo, int 
     return c;
 }
 
-// E > 0: fresh obstacles precomputed in `pre` (E envs, native_obst_draws)
+// E > 0: fresh obstacles precomputed in `pre` (E envs, native_obst_draw)
 template <int A, int O, int E = 0, class Envs, class List>
 __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, const float *form,
                                                     const List &list, int nfin, float cap, int tid,

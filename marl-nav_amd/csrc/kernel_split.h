@@ -183,7 +183,7 @@ struct SplitPlan {
     static constexpr int FTP = (ENVIN + 2 * kWavesPerBlock * EPW + 3) & ~3;
     // then (kSplitSpread shapes with O <= 8, native re-init) the fresh
     // obstacle draws of the workgroup's EW envs, component k of obstacle j of
-    // env code c at PRE + (2j + k) * EW + c (kernel_reinit.h native_obst_draws)
+    // env code c at PRE + (2j + k) * EW + c (native_obst_draw, device_math.h)
     static constexpr int EW = kWavesPerBlock * EPW;
     static constexpr int PRE = (FTP + (kSplitTpl<A, O> ? NCP : 0) + 3) & ~3;
     static constexpr int BLK = PRE + (kSplitSpread<A, O> && O <= 8 ? 2 * O * EW : 0);
@@ -438,19 +438,16 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         KArgsK *kl = kargs_late<kHotKargsOff>();
         if (!kl->a.b.fresh_states) {
             const uint64_t sidx = kl->a.step_idx, g0 = (uint64_t)(kl->a.env_offset + e0);
-            constexpr int NB = (O + 1) / 2;
 #pragma unroll
-            for (int k2 = 0; k2 * 64 < EPW * NB; ++k2) {
+            for (int k2 = 0; k2 * 64 < EPW * O; ++k2) {
                 const int i = (int)lane + 64 * k2;
-                const int cl = i % EPW, jb = i / EPW;
-                if (((k2 + 1) * 64 <= EPW * NB || i < EPW * NB) && cl < ne) {
-                    float v[4];
-                    native_obst_draws(pr.seed, sidx, g0 + cl, jb, pr.obs_range_x, pr.obs_mean_x,
-                                      pr.obs_range_y, pr.obs_mean_y, v);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (2 * jb + k / 2 < O)
-                            pre[(4 * jb + k) * SP::EW + wib * EPW + cl] = v[k];
+                const int cl = i % EPW, j = i / EPW;  // obstacle j of env cl
+                if (((k2 + 1) * 64 <= EPW * O || i < EPW * O) && cl < ne) {
+                    float v[2];
+                    native_obst_draw(pr.seed, sidx, g0 + cl, j, pr.obs_range_x, pr.obs_mean_x,
+                                     pr.obs_range_y, pr.obs_mean_y, v);
+                    pre[(2 * j) * SP::EW + wib * EPW + cl] = v[0];
+                    pre[(2 * j + 1) * SP::EW + wib * EPW + cl] = v[1];
                 }
             }
         }

@@ -41,8 +41,10 @@ def load():
         lib.oracle_observe.restype = None
         lib.oracle_reinit_all.argtypes = [dims_p, par_p, P, P, P, P, ctypes.c_uint64]
         lib.oracle_reinit_all.restype = None
-        lib.oracle_philox4x32_10.argtypes = [P, P, P]
-        lib.oracle_philox4x32_10.restype = None
+        lib.oracle_philox2x32_10.argtypes = [P, ctypes.c_uint32, P]
+        lib.oracle_philox2x32_10.restype = None
+        lib.oracle_native_key.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64]
+        lib.oracle_native_key.restype = ctypes.c_uint32
         lib.oracle_normalize.argtypes = [ctypes.c_int64, ctypes.c_int, P, P, P, P]
         lib.oracle_normalize.restype = None
         lib.oracle_sincos.argtypes = [ctypes.c_float, P, P]
@@ -184,11 +186,16 @@ def reinit_all(dims, params, formation, step_idx):
 
 
 def philox(ctr, key):
+    """Philox2x32-10 of a 2-word counter under a 32-bit key (the native
+    stream's generator)."""
     c = np.ascontiguousarray(ctr, np.uint32)
-    k = np.ascontiguousarray(key, np.uint32)
-    o = np.empty(4, np.uint32)
-    load().oracle_philox4x32_10(_ptr(c), _ptr(k), _ptr(o))
+    o = np.empty(2, np.uint32)
+    load().oracle_philox2x32_10(_ptr(c), int(key), _ptr(o))
     return o
+
+
+def native_key(seed, blk, step):
+    return int(load().oracle_native_key(int(seed), int(blk), int(step)))
 
 
 def sincos(th, which=0):

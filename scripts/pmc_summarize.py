@@ -2,17 +2,8 @@
 import collections, csv, glob, json, os, sys
 out, cfg = sys.argv[1], sys.argv[2]
 acc = collections.defaultdict(list)
-STEP_KERNELS = ("wave_kernel", "tile_kernel", "split_kernel", "block_kernel")
-
-
-def is_step(name):
-    """A step launch, not the observe-only instantiation (the OBS_ONLY
-    template argument: 4th of split_kernel, 3rd of the others)."""
-    if not any(k in name for k in STEP_KERNELS):
-        return False
-    args = name[name.index("<") + 1:name.index(">")].split(",")
-    i = 3 if "split_kernel" in name else 2
-    return len(args) > i and args[i].strip() == "false"
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summarize_lib import is_step  # noqa: E402
 
 dur = []
 for f in sorted(glob.glob(os.path.join(out, "p*", "run_counter_collection.csv"))):

@@ -9,6 +9,7 @@ import pytest
 import torch
 
 from conftest import (OBS_FIELDS, ROOT, RTOL, assert_obs_close, record_angle_stats,
+                      record_threshold_stats,
                       assert_states_close, assert_vec_close, cli_args, env_values, golden, meta)
 
 import oracle as orc
@@ -86,6 +87,7 @@ def test_step_matches_reference_golden(pkg, name):
                          prefix="", where=where)
         record_angle_stats("golden F1", "reference", fields_np(obs),
                            [z["obs_" + f][k] for f in OBS_FIELDS])
+        record_threshold_stats("golden F1 (kernel)", fields_np(obs))
         f0 = fields_np(obs0)
         for f, a in zip(OBS_FIELDS, f0):
             if "distance" in f:  # correctly rounded sqrt: bit-exact
@@ -163,6 +165,7 @@ def test_trace_matches_reference(pkg, name):
                          prefix="", where=where)
         record_angle_stats(f"trace {name}", "reference", fields_np(obs),
                            [z["obs_" + f][k] for f in OBS_FIELDS])
+        record_threshold_stats(f"trace {name} (kernel)", fields_np(obs))
         if k % 100 == 99:
             assert (env._num_trunc, env._num_col, env._num_tar) == (
                 z["num_trunc"][k], z["num_col"][k], z["num_tar"][k]), where
@@ -233,6 +236,25 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
         tot += exp["counters"]
     assert [env._num_trunc, env._num_col, env._num_tar] == tot.tolist()
     assert (tot[1] > 0 or steps < 10) and (tot[0] > 0 or steps < ep)  # terminal paths hit
+
+
+def test_threshold_proximity_native_65536(pkg):
+    """on the headline workload (65 536 x 3 x 3, native
+    re-init, random turns, 100 steps) count the observation entries within
+    4 ulp of a reward / terminal threshold (printed in the summary). Those
+    are the only entries whose flag could differ from the reference's when
+    a bearing or distance is 1-2 ulp away from it; the kernel equals the
+    oracle on all of them (test_native_trajectory_bit_exact_vs_oracle)."""
+    P, A, O = 65536, 3, 3
+    g = torch.Generator().manual_seed(2025)
+    env = make_env(pkg, P, A, O, episode_len=200, seed=4242)
+    for k in range(100):
+        th = (torch.rand(P, A, generator=g) - 0.5) * 0.8
+        acc = (torch.rand(P, A, generator=g) - 0.5) * 1.2
+        obs, rew, term, trunc = env.step(torch.stack([th, acc], 2).to(DEV))
+        if k % 10 == 9:  # every 10th step: 10 x 196 608 rows
+            record_threshold_stats("native 65536x3x3 (kernel, 10 of 100 steps)", fields_np(obs))
+    assert np.isfinite(np_(rew)).all()
 
 
 def test_counters_reset_like_mappo(pkg):

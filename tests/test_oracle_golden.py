@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import (OBS_FIELDS, assert_obs_close, record_angle_stats, assert_states_close, assert_traj_obs_close,
+from conftest import (OBS_FIELDS, assert_obs_close, record_angle_stats, record_threshold_stats, assert_states_close, assert_traj_obs_close,
                       assert_vec_close, cli_args, env_values, golden, manifest, meta)
 
 import oracle as orc
@@ -68,6 +68,8 @@ def test_oracle_step_matches_reference(name, mk):
                          where=where)
         record_angle_stats("oracle F1", "reference", fields,
                            [z["obs_" + f][k] for f in OBS_FIELDS])
+        record_threshold_stats("golden F1 (reference's own outputs)",
+                               [z["obs_" + f][k] for f in OBS_FIELDS])
     assert np.mean(exact_rewards) > 0.95   # agent states: nearly all bit for bit
 
 
@@ -207,6 +209,8 @@ def test_oracle_trace_matches_reference(name, pkg, mk):
                          where=where)
         record_angle_stats(f"oracle trace {name}", "reference", fields,
                            [z["obs_" + f][k] for f in OBS_FIELDS])
+        record_threshold_stats(f"trace {name} (reference's own outputs)",
+                               [z["obs_" + f][k] for f in OBS_FIELDS])
 
 
 def test_config1_known_answers():
@@ -220,16 +224,39 @@ def test_config1_known_answers():
 
 
 def test_philox_known_answer():
-    """Philox4x32-10 known-answer vectors (Salmon et al., SC'11, Random123
-    kat_vectors): counter/key all zero and all ones."""
-    np.testing.assert_array_equal(orc.philox([0, 0, 0, 0], [0, 0]),
-                                  [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8])
+    """Philox2x32-10 (the native stream's generator) against the published
+    known-answer vectors of Random123 (kat_vectors, philox2x32 10): counter /
+    key all zero, all ones, and the digits of pi."""
+    np.testing.assert_array_equal(orc.philox([0, 0], 0), [0xff1dae59, 0x6cd10df2])
     f = 0xffffffff
-    np.testing.assert_array_equal(orc.philox([f, f, f, f], [f, f]),
-                                  [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd])
-    np.testing.assert_array_equal(
-        orc.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0]),
-        [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1])
+    np.testing.assert_array_equal(orc.philox([f, f], f), [0x2c3f628b, 0xab4fd7ad])
+    np.testing.assert_array_equal(orc.philox([0x243f6a88, 0x85a308d3], 0x13198a2e),
+                                  [0xdd7ce038, 0xf62a4c12])
+
+
+def test_native_stream_definition():
+    """The native stream as DESIGN.md §4 defines it: obstacle j of env gid at
+    step s is Philox2x32-10 block j, counter (lo32(gid), lo32(s) ^ hi32(gid) *
+    0x85EBCA77), key native_key(seed, j, s); 24-bit uniforms scaled like the reference's
+    sampler (utils.py:390-398). Checked through oracle_reinit_all, including
+    env ids and steps past 2^32 (their high words enter counter and key)."""
+    import marlnav_amd.environment as envmod
+    pr = envmod.make_cparams(env_values(meta("step_a3o3")), seed=0x123456789ABCDEF)
+    pr.obs_range_x, pr.obs_mean_x, pr.obs_range_y, pr.obs_mean_y = 500.0, 750.0, 250.0, 375.0
+    form = np.zeros(17, np.float32)
+    for gid, step in ((0, 0), (77, 5), ((3 << 32) + 9, (1 << 33) + 4)):
+        _, ob, _ = orc.reinit_all(orc.make_dims(1, 3, 3, env_offset=gid), pr, form, step)
+        for j in range(3):
+            key = orc.native_key(pr.seed, j, step)
+            c1 = (step & 0xffffffff) ^ (((gid >> 32) * 0x85EBCA77) & 0xffffffff)
+            r = orc.philox([gid & 0xffffffff, c1], key)
+            u = (r >> 8).astype(np.float32) * np.float32(2.0 ** -24)
+            x = np.float32(500.0) * (u[0] - np.float32(0.5)) + np.float32(750.0)
+            y = np.float32(250.0) * (u[1] - np.float32(0.5)) + np.float32(375.0)
+            assert (ob[0, j, 0], ob[0, j, 1]) == (x, y), (gid, step, j)
+    # distinct blocks, envs and steps give distinct keys or counters
+    keys = {orc.native_key(pr.seed, j, 0) for j in range(64)}
+    assert len(keys) == 64
 
 
 def test_oracle_sincos_correctly_rounded():
