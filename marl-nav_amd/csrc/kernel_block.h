@@ -436,7 +436,12 @@ __global__ void __launch_bounds__(64 * A)
         int *flg = reinterpret_cast<int *>(lds + BP::FLG);
         const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
         // ---- per-env reductions, terminal logic (wave 0, one lane per env)
-        if (w == 0) {
+        // the per-env wave: wave 0, or (MARLNAV_BLOCK_ENV_ROT) wave blk % A,
+        // so the per-env phases of the blocks sharing a CU spread over its
+        // SIMDs; the others take the re-init items as waves 0..A-2 (rtid)
+        const int pw = MARLNAV_BLOCK_ENV_ROT ? (int)(blk % A) : 0;
+        const int rtid = ((w - pw - 1 + A) % A) * 64 + (int)lane;
+        if (w == pw) {
             if (MARLNAV_ENV_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_ENV_PRIO);  // (A/B builds)
             const bool env_on = l < ne;
             bool fin = false, tr_l = false, co_l = false, ta_l = false;
@@ -460,17 +465,11 @@ __global__ void __launch_bounds__(64 * A)
                 for (int i = 0; i < A; ++i) rv[i] = all_in ? ry[i] : rx[i];
                 STAMPX(0);  // (wave 0: the reward terms read)
                 const float rsum = torch_row_sum_r<A>(rv, [](float x) { return x; });
-                if (!(MARLNAV_AB & 1024))  // (AB 1024: timing only, no per-env stores)
-                out_el(b.reward, e, rsum / (float)A);              // torch.mean (:233)
+                const float rmean = rsum / (float)A;               // torch.mean (:233)
 
                 const float step_num = ee.step_num;
                 const bool truncated = ee.truncated, term_old = ee.term_old;
                 const bool terminated = ee.terminated;
-                if (!(MARLNAV_AB & 1024)) {
-                out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
-                out_el(b.terminated, e, (uint8_t)terminated);
-                out_el(b.truncated, e, (uint8_t)truncated);
-                }
                 fin = ee.fin;
                 if (NOISY && fin) {  // noisy native re-init: serial per env
                     KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -496,8 +495,26 @@ __global__ void __launch_bounds__(64 * A)
                         out_el(kl->a.b.target, 2 * e + 1, tgl[1]);
                     }
                 }
-                if (!(MARLNAV_AB & 1024))
-                out_el(b.step_num, e, fin ? blend_in(step_num, 0.0f) : step_num);
+                const float sn_out = fin ? blend_in(step_num, 0.0f) : step_num;
+                const uint8_t tm_out = (uint8_t)(!term_old && all_in);  // :218-219
+                if (MARLNAV_AB & 1024) {  // (AB 1024: timing only, no per-env stores)
+                } else if (MARLNAV_ENV_OUT && wt && full) {
+                    // written through, 32-bit buffer offsets from the block's
+                    // first env: no dirty L2 lines left for the end-of-launch
+                    // write-back, and no 64-bit address math per store
+                    // (MARLNAV_ENV_OUT, marlnav_debug.h)
+                    wt_st(out_buf(b.reward + e0, 4 * E), 4u * l, rmean);
+                    wt_st(out_buf(b.terminates + e0, E), (uint32_t)l, tm_out);
+                    wt_st(out_buf(b.terminated + e0, E), (uint32_t)l, (uint8_t)terminated);
+                    wt_st(out_buf(b.truncated + e0, E), (uint32_t)l, (uint8_t)truncated);
+                    wt_st(out_buf(b.step_num + e0, 4 * E), 4u * l, sn_out);
+                } else {
+                    out_el(b.reward, e, rmean);
+                    out_el(b.terminates, e, tm_out);
+                    out_el(b.terminated, e, (uint8_t)terminated);
+                    out_el(b.truncated, e, (uint8_t)truncated);
+                    out_el(b.step_num, e, sn_out);
+                }
                 tr_l = truncated;
                 co_l = any_col;
                 ta_l = all_in;
@@ -544,14 +561,14 @@ __global__ void __launch_bounds__(64 * A)
             early = kBlockEarlyOut<A, O> && full && !norm && fm == 0ull;
             if (early && !(MARLNAV_AB & 2))
                 block_store2<E * A * D, E * A * 5, NT - 64>(
-                    gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)), st, tid - 64, wt);
+                    gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)), st, rtid, wt);
             STAMPX(0);
             if (fm && !(MARLNAV_AB & 1)) {
                 STAMPX(1);
                 reinit_reobs_native<A, O, kPre ? E : 0>(kargs_late<kHotKargsOff>(), ev,
                                                         lds + BP::FORM, MaskList{fm},
                                                         (int)__popcll(fm), pr.cap_distance,
-                                                        tid - 64, NT - 64, lds + BP::FRESH);
+                                                        rtid, NT - 64, lds + BP::FRESH);
                 STAMPX(2);
             }
         }

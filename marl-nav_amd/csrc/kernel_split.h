@@ -106,6 +106,22 @@ constexpr bool kSplitRRLeader = !kSplitSpread<A, O> || O <= 8 || MARLNAV_SPLIT_R
 template <int A, int O>
 constexpr bool kSplitTplPass = kSplitTpl<A, O> && (64 * kWavesPerBlock) % O == 0;
 
+// ... and, with one env per wave (A16/O32 at LPR 4), a finished env is
+// re-initialised and re-observed by its own wave right after its
+// observation, before the per-env barrier: its fin is known there (the
+// wave's collision flags, staged step number and `terminates`), and its
+// fresh observation is the formation template plus the fresh obstacles'
+// pairs (8 per lane, one Philox block per obstacle lane), so no workgroup
+// waits for a tail pass after the per-env phase (MARLNAV_SPLIT_OWN_REINIT).
+template <int A, int O, int LPR>
+constexpr bool kSplitOwn = kSplitTplPass<A, O> && 64 / LPR / A == 1 && MARLNAV_SPLIT_OWN_REINIT;
+
+// one env code as a finished-env list (kernel_reinit.h passes)
+struct OneEnv {
+    int c;
+    __device__ int operator[](int) const { return c; }
+};
+
 // Extra LDS cycles of the workgroup-spread row-reward read (kernel_split.h,
 // wave 0, lane = tile cw * R + row rw, reading the row's K bond terms at
 // tile base cw * F + BOND, row stride K, one ds_read_b32 per term): banks are
@@ -556,6 +572,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     const float *tge = wl + SP::TG + 2 * el;
     float *orow = wl + SP::OBS + rowc * SP::DP;
     float *brow = wl + SP::BOND + rowc * (A - 1);
+    bool row_col = false;  // (kSplitOwn) this lane's row collides
     {
         // wave-uniform choice of the pair math (coord_ok);
         // worth its check only when each lane evaluates many pairs
@@ -582,6 +599,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                                                         brow, pr, unused);
         if (!OBS_ONLY) {
             const unsigned fl = lpr_or<LPR>(t.fl);
+            row_col = row_on && (fl & 10u) != 0u;  // ob_col | ag_col of this row
             const int band = lpr_sum<LPR>(t.band);
             wave_sync();  // bond terms of the row are in LDS
             if (row_on && q == 0) {
@@ -599,6 +617,57 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                         row_reward(t.ta, t.td, fl, band, brow);
                 }
             }
+        }
+    }
+    // ---- kSplitOwn: this wave's env, if it finishes (environment.py:96-104,
+    // 213-214: the same test as per_env's), re-initialised (:76-90) and
+    // re-observed (:105) here, on the wave's own lanes. The reward terms of
+    // the old observation are already in RED / BOND for the per-env phase.
+    if constexpr (kSplitOwn<A, O, LPR> && !OBS_ONLY && !NOISY) {
+        const float sn0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn_in), 0));
+        const unsigned tm0 = (unsigned)__builtin_amdgcn_readlane((int)term_in, 0);
+        const bool fin = tpl_on && !(MARLNAV_AB & 1) &&
+                         (sn0 + 1.0f > pr.trunc_after || tm0 != 0u || __ballot(row_col) != 0ull);
+        if (fin) {
+            wave_sync();  // the row leaders' reads of the old rows are done
+            KArgsK *kl = kargs_late<kHotKargsOff>();
+            const float *form = kl->a.b.formation;
+            const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
+                lds, blk0 * EPW};
+            const int c = wib * EPW;
+            const int64_t e = ev.env(c);
+            bool uncl = false;
+            // the state and target blends (0 * old + fresh)
+            for (int k2 = (int)lane; k2 < 5 * A + 2; k2 += 64) {
+                const bool tg = k2 >= 5 * A;
+                float *d = tg ? ev.targ(c) + (k2 - 5 * A) : ev.state(c) + k2;
+                const float vb = blend_in(*d, form[k2]);
+                *d = vb;
+                if (tg) out_el(kl->a.b.target, 2 * e + (k2 - 5 * A), vb);
+                uncl |= (tg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(form[k2]);
+            }
+            // the fresh obstacles: one Philox block per obstacle lane
+            for (int j = (int)lane; j < O; j += 64) {
+                float v[2];
+                native_obst_draw(kl->p.seed, kl->a.step_idx, (uint64_t)(kl->a.env_offset + e), j,
+                                 kl->p.obs_range_x, kl->p.obs_mean_x, kl->p.obs_range_y,
+                                 kl->p.obs_mean_y, v);
+                float *o = ev.obst(c) + 2 * j;
+                o[0] = blend_in(o[0], v[0]);
+                o[1] = blend_in(o[1], v[1]);
+                out_el(kl->a.b.obstacles, e * O * 2 + 2 * j, o[0]);
+                out_el(kl->a.b.obstacles, e * O * 2 + 2 * j + 1, o[1]);
+            }
+            wave_sync();
+            // the fresh observation: template pairs + obstacle pairs, or every
+            // pair when a blend left the formation's bits (a non-finite old
+            // value: the template does not describe the env)
+            if (__ballot(uncl) == 0ull)
+                reobs_block_tpl<A, O>(ev, OneEnv{c}, 1, pr.cap_distance,
+                                      reinterpret_cast<const float2 *>(kl->a.b.formation_obs),
+                                      (int)lane, 64);
+            else
+                reobs_block<A, O>(ev, OneEnv{c}, 1, pr.cap_distance, (int)lane, 64);
         }
     }
     STAMP(3);
@@ -727,14 +796,16 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 #pragma unroll
             for (int i = 0; i < A; ++i) rv[i] = all_in ? rh[i] : rm[i];
             const float rsum = torch_row_sum_r<A>(rv, [](float r) { return r; });
-            out_el(b.reward, e, rsum / (float)A);             // torch.mean (:233)
+            const auto put_f = [&](float *arr, float v) { out_el(arr, e, v); };
+            const auto put_b = [&](uint8_t *arr, uint8_t v) { out_el(arr, e, v); };
+            put_f(b.reward, rsum / (float)A);                  // torch.mean (:233)
             float step_num = sn_v + 1.0f;                      // :96
             const bool truncated = step_num > pr.trunc_after;  // :97
             const bool term_old = term_v != 0u;
             const bool terminated = any_col || term_old;       // :213-214
-            out_el(b.terminates, e, (uint8_t)(!term_old && all_in));  // :218-219
-            out_el(b.terminated, e, (uint8_t)terminated);
-            out_el(b.truncated, e, (uint8_t)truncated);
+            put_b(b.terminates, (uint8_t)(!term_old && all_in));  // :218-219
+            put_b(b.terminated, (uint8_t)terminated);
+            put_b(b.truncated, (uint8_t)truncated);
             const bool fin = truncated || terminated;          // :102-104
             if (fin && (NOISY || !kSplitSpread<A, O>)) {  // per-env re-init on the env lane
                 KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -769,7 +840,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 out_el(gtg, 2 * e + 1, tgl[1]);
             }
             if (fin) step_num = blend_in(step_num, 0.0f);
-            out_el(b.step_num, e, step_num);
+            put_f(b.step_num, step_num);
             tr_l = truncated;
             co_l = any_col;
             ta_l = all_in;
@@ -805,7 +876,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             __syncthreads();
             STAMP(4);
             if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
-            if (wib == 0) {
+            // the wave that runs the workgroup's per-env phase (MARLNAV_SPLIT_ENV_ROT:
+            // rotated by workgroup, so the per-env phases of the workgroups
+            // sharing a CU do not all land on the SIMD of their wave 0)
+            const int envw = (MARLNAV_SPLIT_ENV_ROT && live == kWavesPerBlock)
+                                 ? (int)(blockIdx.x & (kWavesPerBlock - 1)) : 0;
+            if (wib == envw) {
                 // every row of the workgroup: its reward terms (one lane per
                 // row, all 64 lanes busy where the row leaders were 1 in LPR)
                 static_assert(kWavesPerBlock * R <= 64, "one lane per row of the workgroup");
@@ -848,7 +924,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 #if MARLNAV_STAMPS
             stamp_nfin = list.total();
 #endif
-            if (const int nfin = (MARLNAV_AB & 1) ? 0 : list.total()) {  // (AB 1: timing only)
+            // (kSplitOwn with the template: every finished env was re-initialised
+            // and re-observed by its own wave before the per-env barrier)
+            const bool own_done = kSplitOwn<A, O, LPR> && tpl_on;
+            if (const int nfin = ((MARLNAV_AB & 1) || own_done) ? 0 : list.total()) {  // (AB 1: timing only)
                 KArgsK *kl = kargs_late<kHotKargsOff>();
                 const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
                     lds, blk0 * EPW};

@@ -58,6 +58,32 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_ENV_PRIO
 #define MARLNAV_ENV_PRIO 3
 #endif
+// Env-block kernel: wave 0's per-env outputs (reward, terminates,
+// terminated, truncated, step_num; environment.py:96-104, 213-233) of a full
+// block in a written-through launch as written-through buffer stores (1) or
+// as plain stores (0). Same box, graph replay, steady (profiles/r05_ab_envout.txt):
+// 0 -> 1: 65536x3x3 6.84 -> 6.70 us, 16384x3x3 5.01 -> 4.99, 32768x3x3 and
+// 131072x3x8 unchanged. Staging them in LDS and storing them as 16-byte
+// written-through pieces beside the block store instead measured slower
+// (6.94, 5.13, 17.89 us). The split kernel's per-env outputs written through
+// the same way (removed) measured slower: 4096x16x32 11.63 -> 11.80 us,
+// 512x16x32 8.00 -> 8.17, 1024x3x8 4.82 -> 4.90 (profiles/r05_ab_envout_confirm.txt).
+#ifndef MARLNAV_ENV_OUT
+#define MARLNAV_ENV_OUT 1
+#endif
+// Env-block kernel: per-env phase on wave (block % A) instead of wave 0 (A/B builds)
+#ifndef MARLNAV_BLOCK_ENV_ROT
+#define MARLNAV_BLOCK_ENV_ROT 0
+#endif
+// Split kernel, one env per wave (A16/O32): finished envs re-initialised and
+// re-observed by their own wave before the per-env barrier (kSplitOwn)
+#ifndef MARLNAV_SPLIT_OWN_REINIT
+#define MARLNAV_SPLIT_OWN_REINIT 0
+#endif
+// Split kernel: per-env phase on wave (workgroup % 4) instead of wave 0 (A/B builds)
+#ifndef MARLNAV_SPLIT_ENV_ROT
+#define MARLNAV_SPLIT_ENV_ROT 0
+#endif
 // Round-4 A/B variants measured and removed from the sources (in git history
 // at bc24ae1, DESIGN.md §5 "Round 4"): MARLNAV_EARLY_OUT's first forms,
 // MARLNAV_DEFER_BLOCK_ENV_OUT, MARLNAV_TAIL_PRIO (env-block kernel);
