@@ -436,12 +436,7 @@ __global__ void __launch_bounds__(64 * A)
         int *flg = reinterpret_cast<int *>(lds + BP::FLG);
         const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
         // ---- per-env reductions, terminal logic (wave 0, one lane per env)
-        // the per-env wave: wave 0, or (MARLNAV_BLOCK_ENV_ROT) wave blk % A,
-        // so the per-env phases of the blocks sharing a CU spread over its
-        // SIMDs; the others take the re-init items as waves 0..A-2 (rtid)
-        const int pw = MARLNAV_BLOCK_ENV_ROT ? (int)(blk % A) : 0;
-        const int rtid = ((w - pw - 1 + A) % A) * 64 + (int)lane;
-        if (w == pw) {
+        if (w == 0) {
             if (MARLNAV_ENV_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_ENV_PRIO);  // (A/B builds)
             const bool env_on = l < ne;
             bool fin = false, tr_l = false, co_l = false, ta_l = false;
@@ -561,15 +556,17 @@ __global__ void __launch_bounds__(64 * A)
             early = kBlockEarlyOut<A, O> && full && !norm && fm == 0ull;
             if (early && !(MARLNAV_AB & 2))
                 block_store2<E * A * D, E * A * 5, NT - 64>(
-                    gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)), st, rtid, wt);
+                    gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)), st, tid - 64, wt);
             STAMPX(0);
             if (fm && !(MARLNAV_AB & 1)) {
+                if (MARLNAV_REINIT_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_REINIT_PRIO);  // (A/B builds)
                 STAMPX(1);
                 reinit_reobs_native<A, O, kPre ? E : 0>(kargs_late<kHotKargsOff>(), ev,
                                                         lds + BP::FORM, MaskList{fm},
                                                         (int)__popcll(fm), pr.cap_distance,
-                                                        rtid, NT - 64, lds + BP::FRESH);
+                                                        tid - 64, NT - 64, lds + BP::FRESH);
                 STAMPX(2);
+                if (MARLNAV_REINIT_PRIO) __builtin_amdgcn_s_setprio(0);
             }
         }
         __syncthreads();

@@ -106,22 +106,6 @@ constexpr bool kSplitRRLeader = !kSplitSpread<A, O> || O <= 8 || MARLNAV_SPLIT_R
 template <int A, int O>
 constexpr bool kSplitTplPass = kSplitTpl<A, O> && (64 * kWavesPerBlock) % O == 0;
 
-// ... and, with one env per wave (A16/O32 at LPR 4), a finished env is
-// re-initialised and re-observed by its own wave right after its
-// observation, before the per-env barrier: its fin is known there (the
-// wave's collision flags, staged step number and `terminates`), and its
-// fresh observation is the formation template plus the fresh obstacles'
-// pairs (8 per lane, one Philox block per obstacle lane), so no workgroup
-// waits for a tail pass after the per-env phase (MARLNAV_SPLIT_OWN_REINIT).
-template <int A, int O, int LPR>
-constexpr bool kSplitOwn = kSplitTplPass<A, O> && 64 / LPR / A == 1 && MARLNAV_SPLIT_OWN_REINIT;
-
-// one env code as a finished-env list (kernel_reinit.h passes)
-struct OneEnv {
-    int c;
-    __device__ int operator[](int) const { return c; }
-};
-
 // Extra LDS cycles of the workgroup-spread row-reward read (kernel_split.h,
 // wave 0, lane = tile cw * R + row rw, reading the row's K bond terms at
 // tile base cw * F + BOND, row stride K, one ds_read_b32 per term): banks are
@@ -372,6 +356,197 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     return t;
 }
 
+// one env code as a finished-env list (kernel_reinit.h passes)
+struct OneEnv {
+    int c;
+    __device__ int operator[](int) const { return c; }
+};
+
+// ---- one env per wave (A16/O32 at LPR 4): the observation in two passes,
+// so a finished env's wave can skip the bearings of the observation the
+// re-initialisation discards (environment.py:99-105: rows of finished envs
+// are replaced by the fresh env's) and spend them on the fresh env's rows
+// instead, before the per-env barrier (kSplitOwn). Pass 1 computes every
+// pair's distance (kept in registers), the reward flags, band and bond terms
+// exactly as split_pairs does; pass 2 the bearings from those distances (the
+// same pair_angle operations on the same inputs: bit for bit what
+// split_pairs writes).
+template <int A, int O, int LPR>
+constexpr bool kSplitOwn = kSplitTplPass<A, O> && 64 / LPR / A == 1 && MARLNAV_SPLIT_OWN;
+
+template <int A, int O, int LPR>
+struct SplitSlots {
+    using SP = SplitPlan<A, O, LPR>;
+    static constexpr int N = SP::NOB + SP::NAG;
+};
+
+template <int A, int O, int LPR, bool FAST, bool TFAST, bool SHARP1>
+__device__ __forceinline__ SplitTerms split_dists(const float *__restrict__ sts,
+                                                  const float *__restrict__ obe,
+                                                  const float *__restrict__ tge, int a, int q,
+                                                  float ox, float oy, float *__restrict__ bond_row,
+                                                  const MarlnavParams &pr, bool &ok,
+                                                  float (&dst)[SplitSlots<A, O, LPR>::N])
+{
+    using SP = SplitPlan<A, O, LPR>;
+    constexpr int TQ = LPR - 1;
+    SplitTerms t{0u, 0, 0.0f, 0.0f};
+    float ob_min = __builtin_inff(), ag_min = __builtin_inff();
+    static_assert(!TFAST || FAST, "short divisions need the fast coordinate range");
+    DivC d_sharp{1.0f, 1.0f};
+    if constexpr (TFAST && !SHARP1) d_sharp = make_divc(pr.bond_sharpness, ok);
+    if constexpr (!kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>)
+        t.td = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
+#pragma unroll 64
+    for (int i = 0; i < SP::NOB; ++i) {
+        const int j = q + LPR * i;
+        const bool valid = O % LPR == 0 || j < O;
+        const bool tgt = kSplitTgtInOb<A, O, LPR> && i == SP::NOB - 1 && q == TQ;
+        dst[i] = 0.0f;
+        if (valid || tgt) {
+            const float *pt = tgt ? tge : obe + 2 * (valid ? j : 0);
+            const float d = pair_dist<FAST>(ox, oy, pt[0], pt[1], ok);
+            dst[i] = d;
+            if (valid) ob_min = __builtin_fminf(ob_min, d);
+            else t.td = d;
+        }
+    }
+#pragma unroll 64
+    for (int i = 0; i < SP::NAG; ++i) {
+        const int kx = q + LPR * i;
+        const bool valid = (A - 1) % LPR == 0 || kx < A - 1;
+        const bool tgt = kSplitTgtInAg<A, O, LPR> && i == SP::NAG - 1 && q == TQ;
+        dst[SP::NOB + i] = 0.0f;
+        if (valid || tgt) {
+            const int m = valid ? kx + (kx >= a ? 1 : 0) : 0;
+            const float *pt = tgt ? tge : sts + 5 * m;
+            const float d = pair_dist<FAST>(ox, oy, pt[0], pt[1], ok);
+            dst[SP::NOB + i] = d;
+            if (!valid) {
+                t.td = d;
+            } else {
+                ag_min = __builtin_fminf(ag_min, d);
+                t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
+                if constexpr (TFAST) {
+                    const float sd = SHARP1 ? d - pr.ideal_dist : div_c(d - pr.ideal_dist, d_sharp, ok);
+                    bond_row[kx] = recip_fast(1.0f + sd * sd, ok);
+                } else {
+                    const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
+                    bond_row[kx] = 1.0f / (1.0f + sd * sd);
+                }
+            }
+        }
+    }
+    t.fl |= (ob_min < pr.ob_risk_dist ? 1u : 0u) | (ob_min < pr.ob_coll_dist ? 2u : 0u) |
+            (ag_min < pr.ag_risk_dist ? 4u : 0u) | (ag_min < pr.ag_coll_dist ? 8u : 0u);
+    return t;
+}
+
+// Pass 2: the bearings of the pairs of split_dists (all of them, or with
+// TGT_ONLY the target pair alone), written into the row as split_pairs
+// writes them. Returns the target bearing on the lane that holds it.
+template <int A, int O, int LPR, bool FAST, bool TGT_ONLY>
+__device__ __forceinline__ float split_bearings(const float *__restrict__ sts,
+                                                const float *__restrict__ obe,
+                                                const float *__restrict__ tge, int a, int q,
+                                                float ox, float oy, float dx, float dy,
+                                                float *__restrict__ orow, float td,
+                                                const MarlnavParams &pr, bool &ok,
+                                                const float (&dst)[SplitSlots<A, O, LPR>::N])
+{
+    using SP = SplitPlan<A, O, LPR>;
+    constexpr int TQ = LPR - 1;
+    const float cap = pr.cap_distance;
+    float ta = 0.0f;
+    if constexpr (!kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>) {
+        ta = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, td, cap, ok);
+        if (q == 0) {
+            orow[0] = ta;
+            orow[1] = td;
+        }
+    }
+#pragma unroll 64
+    for (int i = 0; i < SP::NOB; ++i) {
+        const int j = q + LPR * i;
+        const bool valid = O % LPR == 0 || j < O;
+        const bool tgt = kSplitTgtInOb<A, O, LPR> && i == SP::NOB - 1 && q == TQ;
+        if ((valid && !TGT_ONLY) || tgt) {
+            const float *pt = tgt ? tge : obe + 2 * (valid ? j : 0);
+            const float ang = pair_angle<FAST>(ox, oy, pt[0], pt[1], dx, dy, dst[i], cap, ok);
+            if (valid) {
+                orow[2 + j] = ang;
+                orow[2 + O + j] = dst[i];
+            } else {
+                orow[0] = ang;
+                orow[1] = dst[i];
+                ta = ang;
+            }
+        }
+    }
+#pragma unroll 64
+    for (int i = 0; i < SP::NAG; ++i) {
+        const int kx = q + LPR * i;
+        const bool valid = (A - 1) % LPR == 0 || kx < A - 1;
+        const bool tgt = kSplitTgtInAg<A, O, LPR> && i == SP::NAG - 1 && q == TQ;
+        if ((valid && !TGT_ONLY) || tgt) {
+            const int m = valid ? kx + (kx >= a ? 1 : 0) : 0;
+            const float *pt = tgt ? tge : sts + 5 * m;
+            const float ang =
+                pair_angle<FAST>(ox, oy, pt[0], pt[1], dx, dy, dst[SP::NOB + i], cap, ok);
+            if (!valid) {
+                orow[0] = ang;
+                orow[1] = dst[SP::NOB + i];
+                ta = ang;
+            } else {
+                orow[2 + 2 * O + kx] = ang;
+                orow[2 + 2 * O + (A - 1) + kx] = dst[SP::NOB + i];
+            }
+        }
+    }
+    return ta;
+}
+
+// The fresh env's row of agent a on this lane's slots (the native
+// re-initialisation, environment.py:76-90, then observations() :105): the
+// fresh agent (fx, fy, fdx, fdy) against the fresh obstacles `obf` (pair
+// math, as reinit_reobs_tpl computes them), the target and other-agent slots
+// from the formation's observation template `tv` (this lane's slots, loaded
+// by the caller: raw bearing, distance; the cap applied here as in
+// reobs_block_tpl).
+template <int A, int O, int LPR, bool FAST>
+__device__ __forceinline__ void split_fresh_row(const float *__restrict__ obf, int q, float fx,
+                                                float fy, float fdx, float fdy,
+                                                float *__restrict__ orow, float cap, bool &ok,
+                                                const float2 (&tv)[SplitPlan<A, O, LPR>::NAG + 1])
+{
+    using SP = SplitPlan<A, O, LPR>;
+    constexpr int TQ = LPR - 1;
+    static_assert(kSplitTgtInAg<A, O, LPR>, "the target in the other-agent loop's spare slot");
+#pragma unroll 64
+    for (int i = 0; i < SP::NOB; ++i) {
+        const int j = q + LPR * i;
+        if (O % LPR == 0 || j < O) {
+            const float px = obf[2 * j], py = obf[2 * j + 1];
+            const float d = pair_dist<FAST>(fx, fy, px, py, ok);
+            orow[2 + j] = pair_angle<FAST>(fx, fy, px, py, fdx, fdy, d, cap, ok);
+            orow[2 + O + j] = d;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < SP::NAG; ++i) {
+        const int kx = q + LPR * i;
+        const bool valid = kx < A - 1;
+        const bool tgt = i == SP::NAG - 1 && q == TQ;
+        if (valid || tgt) {
+            const float2 t = tv[i];
+            const int sa = valid ? 2 + 2 * O + kx : 0;
+            const int sd = valid ? 2 + 2 * O + (A - 1) + kx : 1;
+            orow[sa] = t.y < cap ? 0.0f : t.x;  // the cap (environment.py:172-177)
+            orow[sd] = t.y;
+        }
+    }
+}
+
 template <int A, int O, int LPR, bool OBS_ONLY, bool NOISY>
 // (min 4 waves per SIMD: keeps the max-ilp scheduler (Makefile) within the
 // 128 VGPRs of the 4-waves-per-SIMD grids; unbounded it takes 178 at A16/O32
@@ -572,7 +747,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     const float *tge = wl + SP::TG + 2 * el;
     float *orow = wl + SP::OBS + rowc * SP::DP;
     float *brow = wl + SP::BOND + rowc * (A - 1);
-    bool row_col = false;  // (kSplitOwn) this lane's row collides
     {
         // wave-uniform choice of the pair math (coord_ok);
         // worth its check only when each lane evaluates many pairs
@@ -584,7 +758,116 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         }
         bool unused = true;
         SplitTerms t;
-        if (__builtin_expect(fast, 1) && !OBS_ONLY && (pr.flags & kTermsFastFlag) &&
+        if constexpr (kSplitOwn<A, O, LPR> && !OBS_ONLY) {
+            // ---- kSplitOwn: distances first, the env's finished test, then
+            // the bearings of the observation that stays (or of its target
+            // pair alone) and, for a finished env, its fresh rows
+            float dst[SplitSlots<A, O, LPR>::N];
+            const bool tfast = (pr.flags & kTermsFastFlag) != 0;
+            if (__builtin_expect(fast, 1) && tfast && pr.bond_sharpness == 1.0f)
+                t = split_dists<A, O, LPR, true, true, true>(sts, obe, tge, a, q, ox, oy, brow, pr,
+                                                            unused, dst);
+            else if (__builtin_expect(fast, 1) && tfast)
+                t = split_dists<A, O, LPR, true, true, false>(sts, obe, tge, a, q, ox, oy, brow, pr,
+                                                             unused, dst);
+            else if (__builtin_expect(fast, 1))
+                t = split_dists<A, O, LPR, true, false, false>(sts, obe, tge, a, q, ox, oy, brow,
+                                                              pr, unused, dst);
+            else
+                t = split_dists<A, O, LPR, false, false, false>(sts, obe, tge, a, q, ox, oy, brow,
+                                                               pr, unused, dst);
+            const unsigned fl = lpr_or<LPR>(t.fl);
+            const int band = lpr_sum<LPR>(t.band);
+            // per_env's test (environment.py:96-104, 213-214) on the wave's env:
+            // its step number and `terminates` on lane 0, its rows' collisions
+            const float sn0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn_in), 0));
+            const unsigned tm0 = (unsigned)__builtin_amdgcn_readlane((int)term_in, 0);
+            const bool col = __ballot(row_on && (fl & 10u) != 0u) != 0ull;
+            const bool own_fin = tpl_on && !(MARLNAV_AB & 1) &&
+                                 (sn0 + 1.0f > pr.trunc_after || tm0 != 0u || col);
+            if (!own_fin) {
+                if (__builtin_expect(fast, 1))
+                    split_bearings<A, O, LPR, true, false>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
+                                                           t.td, pr, unused, dst);
+                else
+                    split_bearings<A, O, LPR, false, false>(sts, obe, tge, a, q, ox, oy, dx, dy,
+                                                            orow, t.td, pr, unused, dst);
+            } else {
+                if (__builtin_expect(fast, 1))
+                    split_bearings<A, O, LPR, true, true>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
+                                                          t.td, pr, unused, dst);
+                else
+                    split_bearings<A, O, LPR, false, true>(sts, obe, tge, a, q, ox, oy, dx, dy,
+                                                           orow, t.td, pr, unused, dst);
+            }
+            wave_sync();  // bond terms and the target pair of each row are in LDS
+            if (row_on && q == 0) {
+                t.ta = orow[0];  // computed by lane LPR-1
+                t.td = orow[1];
+                reinterpret_cast<float4 *>(wl + SP::RED)[row] =
+                    make_float4(t.ta, t.td, __uint_as_float(fl), __int_as_float(band));
+            }
+            if (own_fin) {
+                // ---- the fresh env (environment.py:76-90, 104-105) on this
+                // wave: blends of the state and target, the fresh obstacles
+                // (one Philox block per obstacle lane), then its rows - the
+                // formation template's target / other-agent pairs and the
+                // obstacle pairs, or every pair computed when a blend left the
+                // formation's bits (a non-finite old value)
+                wave_sync();  // the row leaders have read the old target pair
+                KArgsK *kl = kargs_late<kHotKargsOff>();
+                const float *form = kl->a.b.formation;
+                const float2 *tpg = reinterpret_cast<const float2 *>(kl->a.b.formation_obs);
+                float2 tv[SplitPlan<A, O, LPR>::NAG + 1];
+#pragma unroll
+                for (int i = 0; i < SplitPlan<A, O, LPR>::NAG; ++i) {  // (loads first)
+                    const int kx = q + LPR * i;
+                    const bool valid = kx < A - 1;
+                    const bool tgt = i == SplitPlan<A, O, LPR>::NAG - 1 && q == LPR - 1;
+                    tv[i] = (valid || tgt) ? tpg[rowc * A + (valid ? kx + 1 : 0)] : make_float2(0.f, 0.f);
+                }
+                tv[SplitPlan<A, O, LPR>::NAG] = make_float2(0.f, 0.f);
+                const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
+                    lds, blk0 * EPW};
+                const int c = wib * EPW;
+                const int64_t e = ev.env(c);
+                bool uncl = false;
+                for (int k2 = (int)lane; k2 < 5 * A + 2; k2 += 64) {
+                    const bool tg = k2 >= 5 * A;
+                    float *d = tg ? ev.targ(c) + (k2 - 5 * A) : ev.state(c) + k2;
+                    const float vb = blend_in(*d, form[k2]);
+                    *d = vb;
+                    if (tg) out_el(kl->a.b.target, 2 * e + (k2 - 5 * A), vb);
+                    uncl |= (tg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(form[k2]);
+                }
+                for (int j = (int)lane; j < O; j += 64) {
+                    float v[2];
+                    native_obst_draw(kl->p.seed, kl->a.step_idx, (uint64_t)(kl->a.env_offset + e),
+                                     j, kl->p.obs_range_x, kl->p.obs_mean_x, kl->p.obs_range_y,
+                                     kl->p.obs_mean_y, v);
+                    float *o = ev.obst(c) + 2 * j;
+                    o[0] = blend_in(o[0], v[0]);
+                    o[1] = blend_in(o[1], v[1]);
+                    out_el(kl->a.b.obstacles, e * O * 2 + 2 * j, o[0]);
+                    out_el(kl->a.b.obstacles, e * O * 2 + 2 * j + 1, o[1]);
+                }
+                wave_sync();
+                if (__ballot(uncl) == 0ull) {
+                    const float *fs = st + 5 * rowc;  // the blended (= formation) agent row
+                    const float fx = fs[0], fy = fs[1], fdx = fs[2], fdy = fs[3];
+                    const bool cok2 = coord_ok(fx) && coord_ok(fy) &&
+                                      tile_coords_ok<EPW * O * 2, 0>(wl + SP::OB, wl + SP::TG, lane);
+                    if (__ballot(!cok2) == 0ull)
+                        split_fresh_row<A, O, LPR, true>(wl + SP::OB, q, fx, fy, fdx, fdy, orow,
+                                                         pr.cap_distance, unused, tv);
+                    else
+                        split_fresh_row<A, O, LPR, false>(wl + SP::OB, q, fx, fy, fdx, fdy, orow,
+                                                          pr.cap_distance, unused, tv);
+                } else {
+                    reobs_block<A, O>(ev, OneEnv{c}, 1, pr.cap_distance, (int)lane, 64);
+                }
+            }
+        } else if (__builtin_expect(fast, 1) && !OBS_ONLY && (pr.flags & kTermsFastFlag) &&
             pr.bond_sharpness == 1.0f)
             t = split_pairs<A, O, LPR, !OBS_ONLY, true, true, true>(sts, obe, tge, a, q, ox, oy, dx,
                                                                    dy, orow, brow, pr, unused);
@@ -597,9 +880,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         else
             t = split_pairs<A, O, LPR, !OBS_ONLY, false>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
                                                         brow, pr, unused);
-        if (!OBS_ONLY) {
+        if (!OBS_ONLY && !kSplitOwn<A, O, LPR>) {
             const unsigned fl = lpr_or<LPR>(t.fl);
-            row_col = row_on && (fl & 10u) != 0u;  // ob_col | ag_col of this row
             const int band = lpr_sum<LPR>(t.band);
             wave_sync();  // bond terms of the row are in LDS
             if (row_on && q == 0) {
@@ -617,57 +899,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                         row_reward(t.ta, t.td, fl, band, brow);
                 }
             }
-        }
-    }
-    // ---- kSplitOwn: this wave's env, if it finishes (environment.py:96-104,
-    // 213-214: the same test as per_env's), re-initialised (:76-90) and
-    // re-observed (:105) here, on the wave's own lanes. The reward terms of
-    // the old observation are already in RED / BOND for the per-env phase.
-    if constexpr (kSplitOwn<A, O, LPR> && !OBS_ONLY && !NOISY) {
-        const float sn0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn_in), 0));
-        const unsigned tm0 = (unsigned)__builtin_amdgcn_readlane((int)term_in, 0);
-        const bool fin = tpl_on && !(MARLNAV_AB & 1) &&
-                         (sn0 + 1.0f > pr.trunc_after || tm0 != 0u || __ballot(row_col) != 0ull);
-        if (fin) {
-            wave_sync();  // the row leaders' reads of the old rows are done
-            KArgsK *kl = kargs_late<kHotKargsOff>();
-            const float *form = kl->a.b.formation;
-            const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
-                lds, blk0 * EPW};
-            const int c = wib * EPW;
-            const int64_t e = ev.env(c);
-            bool uncl = false;
-            // the state and target blends (0 * old + fresh)
-            for (int k2 = (int)lane; k2 < 5 * A + 2; k2 += 64) {
-                const bool tg = k2 >= 5 * A;
-                float *d = tg ? ev.targ(c) + (k2 - 5 * A) : ev.state(c) + k2;
-                const float vb = blend_in(*d, form[k2]);
-                *d = vb;
-                if (tg) out_el(kl->a.b.target, 2 * e + (k2 - 5 * A), vb);
-                uncl |= (tg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(form[k2]);
-            }
-            // the fresh obstacles: one Philox block per obstacle lane
-            for (int j = (int)lane; j < O; j += 64) {
-                float v[2];
-                native_obst_draw(kl->p.seed, kl->a.step_idx, (uint64_t)(kl->a.env_offset + e), j,
-                                 kl->p.obs_range_x, kl->p.obs_mean_x, kl->p.obs_range_y,
-                                 kl->p.obs_mean_y, v);
-                float *o = ev.obst(c) + 2 * j;
-                o[0] = blend_in(o[0], v[0]);
-                o[1] = blend_in(o[1], v[1]);
-                out_el(kl->a.b.obstacles, e * O * 2 + 2 * j, o[0]);
-                out_el(kl->a.b.obstacles, e * O * 2 + 2 * j + 1, o[1]);
-            }
-            wave_sync();
-            // the fresh observation: template pairs + obstacle pairs, or every
-            // pair when a blend left the formation's bits (a non-finite old
-            // value: the template does not describe the env)
-            if (__ballot(uncl) == 0ull)
-                reobs_block_tpl<A, O>(ev, OneEnv{c}, 1, pr.cap_distance,
-                                      reinterpret_cast<const float2 *>(kl->a.b.formation_obs),
-                                      (int)lane, 64);
-            else
-                reobs_block<A, O>(ev, OneEnv{c}, 1, pr.cap_distance, (int)lane, 64);
         }
     }
     STAMP(3);
@@ -876,12 +1107,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             __syncthreads();
             STAMP(4);
             if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
-            // the wave that runs the workgroup's per-env phase (MARLNAV_SPLIT_ENV_ROT:
-            // rotated by workgroup, so the per-env phases of the workgroups
-            // sharing a CU do not all land on the SIMD of their wave 0)
-            const int envw = (MARLNAV_SPLIT_ENV_ROT && live == kWavesPerBlock)
-                                 ? (int)(blockIdx.x & (kWavesPerBlock - 1)) : 0;
-            if (wib == envw) {
+            if (wib == 0) {
                 // every row of the workgroup: its reward terms (one lane per
                 // row, all 64 lanes busy where the row leaders were 1 in LPR)
                 static_assert(kWavesPerBlock * R <= 64, "one lane per row of the workgroup");

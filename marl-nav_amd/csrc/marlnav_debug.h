@@ -71,24 +71,30 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_ENV_OUT
 #define MARLNAV_ENV_OUT 1
 #endif
-// Env-block kernel: per-env phase on wave (block % A) instead of wave 0 (A/B builds)
-#ifndef MARLNAV_BLOCK_ENV_ROT
-#define MARLNAV_BLOCK_ENV_ROT 0
+// Split kernel, one env per wave (A16/O32): observation in two passes, a
+// finished env re-initialised and re-observed by its own wave before the
+// per-env barrier (kSplitOwn, kernel_split.h)
+#ifndef MARLNAV_SPLIT_OWN
+#define MARLNAV_SPLIT_OWN 0
 #endif
-// Split kernel, one env per wave (A16/O32): finished envs re-initialised and
-// re-observed by their own wave before the per-env barrier (kSplitOwn)
-#ifndef MARLNAV_SPLIT_OWN_REINIT
-#define MARLNAV_SPLIT_OWN_REINIT 0
-#endif
-// Split kernel: per-env phase on wave (workgroup % 4) instead of wave 0 (A/B builds)
-#ifndef MARLNAV_SPLIT_ENV_ROT
-#define MARLNAV_SPLIT_ENV_ROT 0
+// Env-block kernel: s_setprio of the re-init waves' pass in blocks with
+// finished envs (0: none; A/B builds)
+#ifndef MARLNAV_REINIT_PRIO
+#define MARLNAV_REINIT_PRIO 0
 #endif
 // Round-4 A/B variants measured and removed from the sources (in git history
 // at bc24ae1, DESIGN.md §5 "Round 4"): MARLNAV_EARLY_OUT's first forms,
 // MARLNAV_DEFER_BLOCK_ENV_OUT, MARLNAV_TAIL_PRIO (env-block kernel);
 // MARLNAV_SPLIT_OVERLAP, MARLNAV_SPLIT_OWN_ENV, MARLNAV_SPLIT_DEFER_ENV_OUT,
 // MARLNAV_SPLIT_ENV_PRIO (split kernel); MARLNAV_DEFER_REINIT_OUT (re-init).
+// Round 5 (DESIGN.md §5 "Round 5"; code in git history at deae14b):
+// MARLNAV_BLOCK_ENV_ROT / MARLNAV_SPLIT_ENV_ROT (the per-env phase on wave
+// block % A / workgroup % 4: no gain, and the general re-init thread index
+// alone changed the block kernel's register allocation, +0.17 us at
+// 65536x3x3), MARLNAV_SPLIT_OWN_REINIT (A16/O32: a finished env re-initialised
+// and re-observed by its own wave before the per-env barrier: bit-exact, but
+// 4096x16x32 11.66 -> 14.51 us, the lone wave's pair chains run one after the
+// other), MARLNAV_SPLIT_ENV_WT.
 // Env-block kernel: blocks with no finished env stream their rows from waves
 // 1..A-1 under the per-env phase (1), after it (0), or by shape (-1: the
 // product's choice, kBlockEarlyOut in kernel_block.h)
