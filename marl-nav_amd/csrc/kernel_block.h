@@ -561,10 +561,12 @@ __global__ void __launch_bounds__(64 * A)
             if (fm && !(MARLNAV_AB & 1)) {
                 if (MARLNAV_REINIT_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_REINIT_PRIO);  // (A/B builds)
                 STAMPX(1);
+                const TailOut tout{b.obstacles, b.target, e0, wt && full};
                 reinit_reobs_native<A, O, kPre ? E : 0>(kargs_late<kHotKargsOff>(), ev,
                                                         lds + BP::FORM, MaskList{fm},
                                                         (int)__popcll(fm), pr.cap_distance,
-                                                        tid - 64, NT - 64, lds + BP::FRESH);
+                                                        tid - 64, NT - 64, lds + BP::FRESH,
+                                                        MARLNAV_TAIL_PTRS ? &tout : nullptr);
                 STAMPX(2);
                 if (MARLNAV_REINIT_PRIO) __builtin_amdgcn_s_setprio(0);
             }

@@ -338,9 +338,34 @@ __device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, con
 }
 
 // template / obstacle item k2 (< NREST) of finished env c (PRE as above)
+// TailOut (MARLNAV_TAIL_PTRS, A/B builds): the global obstacles / target of
+// the block's envs from the caller's SGPR pointers (0: kernarg loads), and
+// (2) written through with offsets from the block's first env.
+struct TailOut {
+    float *gob, *gtg;
+    int64_t e0;
+    bool wt;
+};
+
+template <int O>
+__device__ __forceinline__ void tail_out(const TailOut *to, KArgsK *kl, bool obst, int64_t idx,
+                                         float v)
+{
+    if (to == nullptr) {
+        out_el(obst ? kl->a.b.obstacles : kl->a.b.target, idx, v);
+    } else if (MARLNAV_TAIL_PTRS == 2 && kWtOut && to->wt) {
+        const int64_t base = obst ? to->e0 * O * 2 : to->e0 * 2;
+        const uint32_t span = obst ? 64u * O * 2 * 4 : 64u * 2 * 4;
+        wt_st(out_buf((obst ? to->gob : to->gtg) + base, span), (uint32_t)(idx - base) * 4u, v);
+    } else {
+        out_el(obst ? to->gob : to->gtg, idx, v);
+    }
+}
+
 template <int A, int O, int E, class Envs>
 __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, const float *form,
-                                                 const float *pre, int c, int k2)
+                                                 const float *pre, int c, int k2,
+                                                 const TailOut *to = nullptr)
 {
     const int64_t e = ev.env(c);
     if (k2 < 5 * A) {
@@ -351,7 +376,7 @@ __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, con
         float *d = ev.targ(c) + j;
         const float v = blend_in(*d, form[k2]);
         *d = v;
-        out_el(kl->a.b.target, 2 * e + j, v);
+        tail_out<O>(to, kl, false, 2 * e + j, v);
     } else {
         const int j = k2 - (5 * A + 2);  // obstacle j
         float v[2];
@@ -363,13 +388,12 @@ __device__ __forceinline__ void native_rest_item(KArgsK *kl, const Envs &ev, con
                              kl->p.obs_range_x, kl->p.obs_mean_x, kl->p.obs_range_y,
                              kl->p.obs_mean_y, v);
         }
-        float *gob = kl->a.b.obstacles;
         float *o = ev.obst(c) + 2 * j;
         const int64_t g = e * O * 2 + 2 * j;
         o[0] = blend_in(o[0], v[0]);
         o[1] = blend_in(o[1], v[1]);
-        out_el(gob, g, o[0]);
-        out_el(gob, g + 1, o[1]);
+        tail_out<O>(to, kl, true, g, o[0]);
+        tail_out<O>(to, kl, true, g + 1, o[1]);
     }
 }
 
@@ -504,7 +528,8 @@ __device__ __forceinline__ int list_code(const MaskList &l, int fe, int lo, int 
 template <int A, int O, int E = 0, class Envs, class List>
 __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, const float *form,
                                                     const List &list, int nfin, float cap, int tid,
-                                                    int nt, const float *pre = nullptr)
+                                                    int nt, const float *pre = nullptr,
+                                                    const TailOut *to = nullptr)
 {
     using IT = NativeItems<A, O>;
     constexpr int NI = IT::NPAIR + IT::NREST;
@@ -513,6 +538,7 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
     if (nwv >= 2) {
         const int pw = nwv >> 1;  // waves [0, pw): pair items; [pw, nwv): the rest
         if (wv < pw) {
+            if (MARLNAV_AB & (1 << 18)) return;  // (timing only: no pair items)
             const int n = nfin * IT::NPAIR;
             for (int base = 64 * wv; base < n; base += 64 * pw) {
                 const int i = base + lane;
@@ -524,13 +550,14 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
                                           ic - fe * IT::NPAIR, on, cap);
             }
         } else {
+            if (MARLNAV_AB & (1 << 17)) return;  // (timing only: no template / obstacle items)
             const int n = nfin * IT::NREST;
             for (int base = 64 * (wv - pw); base < n; base += 64 * (nwv - pw)) {
                 const int i = base + lane;
                 const int lo = base / IT::NREST, hi = min((base + 63) / IT::NREST, nfin - 1);
                 const int fe = (i < n ? i : 0) / IT::NREST;
                 const int c = list_code(list, fe, lo, hi);
-                if (i < n) native_rest_item<A, O, E>(kl, ev, form, pre, c, i - fe * IT::NREST);
+                if (i < n) native_rest_item<A, O, E>(kl, ev, form, pre, c, i - fe * IT::NREST, to);
             }
         }
         return;
@@ -545,6 +572,6 @@ __device__ __forceinline__ void reinit_reobs_native(KArgsK *kl, const Envs &ev, 
         if (kk < IT::NPAIR)
             native_pair_item<A, O, E>(kl, ev, form, pre, c, kk, on, cap);
         else if (on)
-            native_rest_item<A, O, E>(kl, ev, form, pre, c, kk - IT::NPAIR);
+            native_rest_item<A, O, E>(kl, ev, form, pre, c, kk - IT::NPAIR, to);
     }
 }

@@ -371,8 +371,15 @@ struct OneEnv {
 // exactly as split_pairs does; pass 2 the bearings from those distances (the
 // same pair_angle operations on the same inputs: bit for bit what
 // split_pairs writes).
+// The shapes that can run it (kSplitOwn: the instantiation that does,
+// split_kernel's OWN; marlnav_step picks it for grids of at most
+// kSplitOwnMaxEnvs envs, where it measured faster - at four waves per SIMD
+// the SIMDs are VALU-saturated and moving a finished env's work from the
+// workgroup's tail into its wave's observation saves no issue time).
 template <int A, int O, int LPR>
-constexpr bool kSplitOwn = kSplitTplPass<A, O> && 64 / LPR / A == 1 && MARLNAV_SPLIT_OWN;
+constexpr bool kSplitOwnShape = kSplitTplPass<A, O> && 64 / LPR / A == 1;
+template <int A, int O, int LPR, bool OWN>
+constexpr bool kSplitOwn = kSplitOwnShape<A, O, LPR> && (OWN || MARLNAV_SPLIT_OWN);
 
 template <int A, int O, int LPR>
 struct SplitSlots {
@@ -547,7 +554,7 @@ __device__ __forceinline__ void split_fresh_row(const float *__restrict__ obf, i
     }
 }
 
-template <int A, int O, int LPR, bool OBS_ONLY, bool NOISY>
+template <int A, int O, int LPR, bool OBS_ONLY, bool NOISY, bool OWN = false>
 // (min 4 waves per SIMD: keeps the max-ilp scheduler (Makefile) within the
 // 128 VGPRs of the 4-waves-per-SIMD grids; unbounded it takes 178 at A16/O32
 // and halves occupancy)
@@ -758,7 +765,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         }
         bool unused = true;
         SplitTerms t;
-        if constexpr (kSplitOwn<A, O, LPR> && !OBS_ONLY) {
+        if constexpr (kSplitOwn<A, O, LPR, OWN> && !OBS_ONLY) {
             // ---- kSplitOwn: distances first, the env's finished test, then
             // the bearings of the observation that stays (or of its target
             // pair alone) and, for a finished env, its fresh rows
@@ -880,7 +887,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         else
             t = split_pairs<A, O, LPR, !OBS_ONLY, false>(sts, obe, tge, a, q, ox, oy, dx, dy, orow,
                                                         brow, pr, unused);
-        if (!OBS_ONLY && !kSplitOwn<A, O, LPR>) {
+        if (!OBS_ONLY && !kSplitOwn<A, O, LPR, OWN>) {
             const unsigned fl = lpr_or<LPR>(t.fl);
             const int band = lpr_sum<LPR>(t.band);
             wave_sync();  // bond terms of the row are in LDS
@@ -1108,6 +1115,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             STAMP(4);
             if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
             if (wib == 0) {
+                if (MARLNAV_SPLIT_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_SPLIT_PRIO);  // (A/B builds)
                 // every row of the workgroup: its reward terms (one lane per
                 // row, all 64 lanes busy where the row leaders were 1 in LPR)
                 static_assert(kWavesPerBlock * R <= 64, "one lane per row of the workgroup");
@@ -1142,6 +1150,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 c_col = __popcll(__ballot(co_l));
                 c_tar = __popcll(__ballot(ta_l));
                 STAMPX(1);
+                if (MARLNAV_SPLIT_PRIO) __builtin_amdgcn_s_setprio(0);
             }
             __syncthreads();
             STAMPX(2);
@@ -1152,7 +1161,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 #endif
             // (kSplitOwn with the template: every finished env was re-initialised
             // and re-observed by its own wave before the per-env barrier)
-            const bool own_done = kSplitOwn<A, O, LPR> && tpl_on;
+            const bool own_done = kSplitOwn<A, O, LPR, OWN> && tpl_on;
             if (const int nfin = ((MARLNAV_AB & 1) || own_done) ? 0 : list.total()) {  // (AB 1: timing only)
                 KArgsK *kl = kargs_late<kHotKargsOff>();
                 const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{

@@ -75,7 +75,20 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // finished env re-initialised and re-observed by its own wave before the
 // per-env barrier (kSplitOwn, kernel_split.h)
 #ifndef MARLNAV_SPLIT_OWN
-#define MARLNAV_SPLIT_OWN 0
+#define MARLNAV_SPLIT_OWN 0  // 1: the default split instantiation too (A/B builds)
+#endif
+#ifndef MARLNAV_SPLIT_OWN_OFF
+#define MARLNAV_SPLIT_OWN_OFF 0  // 1: never pick the kSplitOwn instantiation (A/B builds)
+#endif
+// Env-block kernel: the finished-env pass's obstacle / target stores through
+// the block's SGPR pointers (1) and written through (2) instead of kernarg
+// loads and plain stores (0) (A/B builds)
+#ifndef MARLNAV_TAIL_PTRS
+#define MARLNAV_TAIL_PTRS 0
+#endif
+// Split kernel: s_setprio of wave 0's row rewards and per-env phase (A/B builds)
+#ifndef MARLNAV_SPLIT_PRIO
+#define MARLNAV_SPLIT_PRIO 0
 #endif
 // Env-block kernel: s_setprio of the re-init waves' pass in blocks with
 // finished envs (0: none; A/B builds)

@@ -230,13 +230,15 @@ struct SplitVariant {
     size_t lds;
     bool always;  // also for large grids
     int lpr;
+    BlockFn step_own;  // kSplitOwn instantiation (one env per wave), or null
 };
 
 #define MARLNAV_SPLIT_VARIANT(A, O, LPR, ALWAYS)                                          \
     {A, O, SplitPlan<A, O, LPR>::EPW, split_kernel<A, O, LPR, false, false>,             \
      split_kernel<A, O, LPR, true, false>, split_kernel<A, O, LPR, false, true>,         \
      (size_t)(SplitPlan<A, O, LPR>::FLOATS * kWavesPerBlock + SplitPlan<A, O, LPR>::BLK) * 4, \
-     ALWAYS, LPR}
+     ALWAYS, LPR,                                                                        \
+     kSplitOwnShape<A, O, LPR> ? split_kernel<A, O, LPR, false, false, true> : nullptr}
 const SplitVariant kSplitVariants[] = {
     MARLNAV_SPLIT_VARIANT(16, 32, 4, true),
     MARLNAV_SPLIT_VARIANT(3, 8, 4, false),
@@ -248,6 +250,12 @@ const SplitVariant kSplitVariants[] = {
     MARLNAV_SPLIT_VARIANT(3, 3, 8, false),
 };
 constexpr int64_t kSplitTinyWaves = 256;
+// kSplitOwn (a finished env re-initialised by its own wave) for grids of at
+// most two waves per SIMD (one env per wave): same box, graph replay,
+// steady (profiles/r05_ab_tail_own2.txt, r05_ab_tail_ablate.txt): 512x16x32
+// 7.98 -> 7.44 us, 1024x16x32 8.28 -> 7.58, 2048x16x32 9.27 -> 8.48;
+// 4096x16x32 (four waves per SIMD) 11.59-11.62 -> 11.65-11.67
+constexpr int64_t kSplitOwnMaxEnvs = 2048;
 #undef MARLNAV_SPLIT_VARIANT
 
 // one-lane-per-row grids below kSplitBelowWaves * (pairs per row / 6) waves
@@ -528,7 +536,10 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
     if (family_allowed(MARLNAV_FAMILY_SPLIT))
         if (const SplitVariant *v = select_split(d, args.b, false, fsplit)) {
             g_last_family = MARLNAV_FAMILY_SPLIT;
-            return launch_split(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
+            const bool own = !noisy && v->step_own && d->num_parallel <= kSplitOwnMaxEnvs &&
+                             !MARLNAV_SPLIT_OWN_OFF;
+            return launch_split(*v, noisy ? v->noisy : (own ? v->step_own : v->step), args, *pr,
+                                stream, "marlnav_step");
         }
     if (family_allowed(MARLNAV_FAMILY_BLOCK))
         if (const BlockVariant *v = select_block(d, args.b, false)) {
