@@ -561,12 +561,16 @@ __global__ void __launch_bounds__(64 * A)
             if (fm && !(MARLNAV_AB & 1)) {
                 if (MARLNAV_REINIT_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_REINIT_PRIO);  // (A/B builds)
                 STAMPX(1);
-                const TailOut tout{b.obstacles, b.target, e0, wt && full};
+                // kTailOut: the pass's obstacle / target outputs through the
+                // block's SGPR pointers, written through (no dirty L2 lines
+                // for the end-of-launch write-back)
+                constexpr int kTailOut = MARLNAV_TAIL_PTRS >= 0 ? MARLNAV_TAIL_PTRS : (kPre ? 2 : 0);
+                const TailOut tout{b.obstacles, b.target, e0, kTailOut == 2 && wt && full};
                 reinit_reobs_native<A, O, kPre ? E : 0>(kargs_late<kHotKargsOff>(), ev,
                                                         lds + BP::FORM, MaskList{fm},
                                                         (int)__popcll(fm), pr.cap_distance,
                                                         tid - 64, NT - 64, lds + BP::FRESH,
-                                                        MARLNAV_TAIL_PTRS ? &tout : nullptr);
+                                                        kTailOut ? &tout : nullptr);
                 STAMPX(2);
                 if (MARLNAV_REINIT_PRIO) __builtin_amdgcn_s_setprio(0);
             }

@@ -338,9 +338,10 @@ __device__ __forceinline__ void native_pair_item(KArgsK *kl, const Envs &ev, con
 }
 
 // template / obstacle item k2 (< NREST) of finished env c (PRE as above)
-// TailOut (MARLNAV_TAIL_PTRS, A/B builds): the global obstacles / target of
-// the block's envs from the caller's SGPR pointers (0: kernarg loads), and
-// (2) written through with offsets from the block's first env.
+// TailOut (the env-block kernel's kTailOut): the global obstacles / target of
+// the block's envs from the caller's SGPR pointers (instead of kernarg
+// loads) and, with `wt`, written through with offsets from the block's
+// first env.
 struct TailOut {
     float *gob, *gtg;
     int64_t e0;
@@ -353,7 +354,7 @@ __device__ __forceinline__ void tail_out(const TailOut *to, KArgsK *kl, bool obs
 {
     if (to == nullptr) {
         out_el(obst ? kl->a.b.obstacles : kl->a.b.target, idx, v);
-    } else if (MARLNAV_TAIL_PTRS == 2 && kWtOut && to->wt) {
+    } else if (kWtOut && to->wt) {
         const int64_t base = obst ? to->e0 * O * 2 : to->e0 * 2;
         const uint32_t span = obst ? 64u * O * 2 * 4 : 64u * 2 * 4;
         wt_st(out_buf((obst ? to->gob : to->gtg) + base, span), (uint32_t)(idx - base) * 4u, v);

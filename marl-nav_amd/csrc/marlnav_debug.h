@@ -81,10 +81,15 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #define MARLNAV_SPLIT_OWN_OFF 0  // 1: never pick the kSplitOwn instantiation (A/B builds)
 #endif
 // Env-block kernel: the finished-env pass's obstacle / target stores through
-// the block's SGPR pointers (1) and written through (2) instead of kernarg
-// loads and plain stores (0) (A/B builds)
+// the block's SGPR pointers (1), also written through (2), or through kernarg
+// loads as plain stores (0); -1: 2 where the fresh obstacles are drawn at
+// stage time (O <= A), else 0. Same box, graph replay, steady
+// (profiles/r05_ab_tp2rp.txt): 0 -> 2: 16384x3x3 5.01 -> 4.89 us, 32768x3x3
+// 5.70 -> 5.55, 65536x3x3 6.70 -> 6.70, 131072x3x8 17.12 -> 17.89 (its
+// 16 obstacle stores per finished env written through); 0 -> 1: 65536x3x3
+// 6.72 -> 6.83 (profiles/r05_ab_tp_sprio_own.txt).
 #ifndef MARLNAV_TAIL_PTRS
-#define MARLNAV_TAIL_PTRS 0
+#define MARLNAV_TAIL_PTRS -1
 #endif
 // Split kernel: s_setprio of wave 0's row rewards and per-env phase (A/B builds)
 #ifndef MARLNAV_SPLIT_PRIO
