@@ -91,7 +91,7 @@ typedef struct MarlnavParams {
     float act_scale[2], act_mean[2];
     uint32_t flags;
     uint32_t reserved;
-    uint64_t seed;           /* native RNG key (Philox4x32-10) */
+    uint64_t seed;           /* native RNG key (Philox2x32-10) */
 } MarlnavParams;
 
 typedef struct MarlnavStepBuffers {
