@@ -1011,6 +1011,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         }
     };
 
+    bool stored = false;  // (the tile went out before the per-env barrier)
     if (!OBS_ONLY) {
         wave_sync();
         // ---- per-env reductions, terminal logic, masked re-init (env e,
@@ -1110,6 +1111,15 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             if (env_on) {
                 bsn[wib * EPW + (int)lane] = sn_in;
                 bterm[wib * EPW + (int)lane] = term_in;
+            }
+            if constexpr (MARLNAV_SPLIT_EARLY && kSplitOwn<A, O, LPR, OWN>) {
+                // own-wave re-init: the tile (rows and states) is final here,
+                // so it streams out under wave 0's per-env phase
+                if (tpl_on && !(MARLNAV_AB & 2)) {
+                    wave_sync();
+                    store_tile();
+                    stored = true;
+                }
             }
             __syncthreads();
             STAMP(4);
@@ -1238,7 +1248,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     // ---- stream the tile out (obs rows and states from LDS)
     wave_sync();
     if (MARLNAV_AB & 2) return;  // (AB 2: timing only - no store)
-    store_tile();
+    if (!stored) store_tile();
     STAMP(6);
     if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
         KArgsK *kl = kargs_late<kHotKargsOff>();
