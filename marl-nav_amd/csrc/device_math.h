@@ -277,31 +277,35 @@ __device__ __forceinline__ DivC make_divc(float c, bool &ok)
 __device__ __forceinline__ float div_c(float x, DivC d, bool &ok)
 {
     ok &= mag_ok(x, 0x1p-70f, 0x1p70f);
-    float q = x * d.r;
-    q = __builtin_fmaf(__builtin_fmaf(-d.c, q, x), d.r, q);
+    const float q = x * d.r;
     return __builtin_fmaf(__builtin_fmaf(-d.c, q, x), d.r, q);
 }
 
-// 1 / den for den in [1, 2^96] (the bond term's 1 + sd^2): div2_fast's core.
+// 1 / den for den in [1, 2^96] (the bond term's 1 + sd^2): v_rcp_f32 and one
+// Newton step, which is the correctly rounded reciprocal for every fp32
+// significand (scripts/probes/div_exhaustive.hip, check R), hence for every
+// den of the range.
 __device__ __forceinline__ float recip_fast(float den, bool &ok)
 {
     ok &= den <= 0x1p96f;
-    float r = __builtin_amdgcn_rcpf(den);
-    r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
-    const float q = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
-    return __builtin_fmaf(__builtin_fmaf(-den, q, 1.0f), r, q);
+    const float r = __builtin_amdgcn_rcpf(den);
+    return __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
 }
 
-// Two correctly rounded quotients over one denominator. This is hipcc's own
-// IEEE fp32 division sequence (reciprocal refined by one Newton step, two
-// residual corrections) with the v_div_scale / v_div_fixup range steps
-// dropped and the reciprocal shared. Those steps only matter when a quotient,
-// reciprocal or residual leaves the normal range; the guard keeps every
-// intermediate normal: den in [2^-60, 2^60] (den is a pair distance clamped
-// at 1e-12, so |x|, |y| <= den) and numerators zero or >= 2^-60 in magnitude.
-// `ok` is cleared otherwise and the caller redoes the row with IEEE division.
-// Branch-free, so consecutive pairs interleave. Checked bit-exact against
-// IEEE division on the GPU: scripts/probes/fastmath_probe.hip.
+// Two correctly rounded quotients over one denominator: v_rcp_f32 refined by
+// one Newton step (r = RN(1/den) for every significand), q = RN(x r), and ONE
+// residual correction q + r (x - den q). hipcc's IEEE sequence applies the
+// correction twice and adds the v_div_scale / v_div_fixup range steps; the
+// second correction never changes the result - checked exhaustively on the
+// GPU over all 2^46 significand pairs (scripts/probes/div_exhaustive.hip:
+// 0 of 7.04e13 differ from x / den; profiles/r05_div_exhaustive.txt) - and
+// the range steps only matter when a quotient, reciprocal or residual leaves
+// the normal range, where the sequence is no longer scale-invariant. The
+// guard keeps every intermediate normal: den in [2^-60, 2^60] (den is a pair
+// distance clamped at 1e-12, so |x|, |y| <= den) and numerators zero or
+// >= 2^-60 in magnitude; `ok` is cleared otherwise and the caller redoes the
+// row with IEEE division. Branch-free, so consecutive pairs interleave.
+// Also sampled against IEEE division: scripts/probes/fastmath_probe.hip.
 __device__ __forceinline__ void div2_fast(float x, float y, float den, float *qx, float *qy,
                                           bool &ok)
 {
@@ -309,12 +313,9 @@ __device__ __forceinline__ void div2_fast(float x, float y, float den, float *qx
           mag_ok(y, 0x1p-60f, 0x1p60f);
     float r = __builtin_amdgcn_rcpf(den);
     r = __builtin_fmaf(__builtin_fmaf(-den, r, 1.0f), r, r);
-    float q = x * r;
-    q = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
+    const float q = x * r, p = y * r;
     *qx = __builtin_fmaf(__builtin_fmaf(-den, q, x), r, q);
-    q = y * r;
-    q = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
-    *qy = __builtin_fmaf(__builtin_fmaf(-den, q, y), r, q);
+    *qy = __builtin_fmaf(__builtin_fmaf(-den, p, y), r, p);
 }
 
 // acos of the bearing (environment.py:286): the device library's acosf
