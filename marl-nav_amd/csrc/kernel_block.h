@@ -423,7 +423,14 @@ __global__ void __launch_bounds__(64 * A)
     __syncthreads();
     STAMP(3);
     if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
-    float *gobs = in_sgpr(b.obs + e0 * (A * D));
+    // the output pointers, read again from the kernarg segment here: no
+    // scalar register holds them through the observation, where the entry
+    // copies spilled 14 SGPRs to VGPR lanes (65536x3x3 6.55 -> 6.33 us,
+    // profiles/r05_ab_late_ptrs.txt; MARLNAV_LATE_PTRS=0: the entry copies)
+    StepPtrs bo;
+    if constexpr (MARLNAV_LATE_PTRS) bo = load_ptrs(kargs_late<kHotKargsOff>());
+    else bo = b;
+    float *gobs = in_sgpr(bo.obs + e0 * (A * D));
     if (OBS_ONLY) block_store(gobs, obs_rows, nrow * D, tid, NT, wt);
     const bool norm = !OBS_ONLY && (pr.flags & MARLNAV_WRITE_OBS_NORM);
     // kBlockEarlyOut: a block with no finished env streams its rows and
@@ -498,17 +505,17 @@ __global__ void __launch_bounds__(64 * A)
                     // first env: no dirty L2 lines left for the end-of-launch
                     // write-back, and no 64-bit address math per store
                     // (MARLNAV_ENV_OUT, marlnav_debug.h)
-                    wt_st(out_buf(b.reward + e0, 4 * E), 4u * l, rmean);
-                    wt_st(out_buf(b.terminates + e0, E), (uint32_t)l, tm_out);
-                    wt_st(out_buf(b.terminated + e0, E), (uint32_t)l, (uint8_t)terminated);
-                    wt_st(out_buf(b.truncated + e0, E), (uint32_t)l, (uint8_t)truncated);
-                    wt_st(out_buf(b.step_num + e0, 4 * E), 4u * l, sn_out);
+                    wt_st(out_buf(bo.reward + e0, 4 * E), 4u * l, rmean);
+                    wt_st(out_buf(bo.terminates + e0, E), (uint32_t)l, tm_out);
+                    wt_st(out_buf(bo.terminated + e0, E), (uint32_t)l, (uint8_t)terminated);
+                    wt_st(out_buf(bo.truncated + e0, E), (uint32_t)l, (uint8_t)truncated);
+                    wt_st(out_buf(bo.step_num + e0, 4 * E), 4u * l, sn_out);
                 } else {
-                    out_el(b.reward, e, rmean);
-                    out_el(b.terminates, e, tm_out);
-                    out_el(b.terminated, e, (uint8_t)terminated);
-                    out_el(b.truncated, e, (uint8_t)truncated);
-                    out_el(b.step_num, e, sn_out);
+                    out_el(bo.reward, e, rmean);
+                    out_el(bo.terminates, e, tm_out);
+                    out_el(bo.terminated, e, (uint8_t)terminated);
+                    out_el(bo.truncated, e, (uint8_t)truncated);
+                    out_el(bo.step_num, e, sn_out);
                 }
                 tr_l = truncated;
                 co_l = any_col;
@@ -556,7 +563,7 @@ __global__ void __launch_bounds__(64 * A)
             early = kBlockEarlyOut<A, O> && full && !norm && fm == 0ull;
             if (early && !(MARLNAV_AB & 2))
                 block_store2<E * A * D, E * A * 5, NT - 64>(
-                    gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)), st, tid - 64, wt);
+                    gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)), st, tid - 64, wt);
             STAMPX(0);
             if (fm && !(MARLNAV_AB & 1)) {
                 if (MARLNAV_REINIT_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_REINIT_PRIO);  // (A/B builds)
@@ -565,7 +572,7 @@ __global__ void __launch_bounds__(64 * A)
                 // block's SGPR pointers, written through (no dirty L2 lines
                 // for the end-of-launch write-back)
                 constexpr int kTailOut = MARLNAV_TAIL_PTRS >= 0 ? MARLNAV_TAIL_PTRS : (kPre ? 2 : 0);
-                const TailOut tout{b.obstacles, b.target, e0, kTailOut == 2 && wt && full};
+                const TailOut tout{bo.obstacles, bo.target, e0, kTailOut == 2 && wt && full};
                 reinit_reobs_native<A, O, kPre ? E : 0>(kargs_late<kHotKargsOff>(), ev,
                                                         lds + BP::FORM, MaskList{fm},
                                                         (int)__popcll(fm), pr.cap_distance,
@@ -592,7 +599,7 @@ __global__ void __launch_bounds__(64 * A)
     STAMP(5);
     if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
         if (!(MARLNAV_AB & 2) && !early)
-        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)),
+        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)),
                                                st, tid, wt);  // (E = 64: whole 16-byte pieces)
     } else if (!OBS_ONLY && full && NT % D == 0) {
         // ---- the same with the fused ObsNormalizer (utils.py:519-532):

@@ -77,6 +77,9 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_SPLIT_OWN
 #define MARLNAV_SPLIT_OWN 0  // 1: the default split instantiation too (A/B builds)
 #endif
+#ifndef MARLNAV_LATE_PTRS
+#define MARLNAV_LATE_PTRS 1  // 0: block kernel output pointers held from the entry (A/B builds)
+#endif
 #ifndef MARLNAV_SPLIT_EARLY
 #define MARLNAV_SPLIT_EARLY 1  // 0: own-wave split tiles stored after the per-env phase (A/B builds;
                                // early: 8.38 vs 8.48 us at 2048x16x32, profiles/r05_ab_early.txt)
