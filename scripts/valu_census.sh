@@ -5,6 +5,7 @@
 # truncation builds of scripts/build_variant.sh (AB 4096 entry, 8192 staged,
 # 16384 observed, 2 all but the block store) and the full kernel; the
 # per-phase shares are the differences (scripts/census_summarize.py).
+#   (PMC_SET=fetch: instruction-fetch and I-cache counters instead)
 #   CFG=65536x3x3 bash scripts/valu_census.sh full:marl-nav_amd/lib/libmarlnav.so ab2:marl-nav_amd/lib/ab2.so
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -15,6 +16,12 @@ PASSES=(
  "SQ_WAVES SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT"
  "SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH SQ_WAVE_CYCLES"
 )
+if [ "${PMC_SET:-}" = fetch ]; then  # instruction-fetch census (code size, I-cache)
+PASSES=(
+ "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_IFETCH"
+ "SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD"
+)
+fi
 for spec in "$@"; do
   tag=${spec%%:*}; lib=${spec#*:}
   OUT=gpurun_out/census_${CFG}/$tag
