@@ -216,6 +216,17 @@ int marlnav_debug_last_family(void);
  * compares it with the oracle's restatement over every fp32 in [-1, 1]). */
 int marlnav_debug_acos_range(uint32_t first, int64_t n, float *out, void *stream);
 
+/* Testing hook (not part of the reference's interface): the step kernels'
+ * short fp32 division sequences (one Newton step, one residual correction:
+ * the normalisation's two quotients, the reward terms' divisions by a
+ * parameter, the bond term's reciprocal) against IEEE division, for the nd
+ * divisor significands d_first + k * d_stride in [1, 2) and every dividend
+ * significand; adds the mismatch counts to the device array out[3]
+ * (quotients, parameter divisions, reciprocals). All-zero over the 2^23
+ * divisors is the exhaustive proof (scripts/probes/div_exhaustive.hip). */
+int marlnav_debug_fastdiv_check(uint32_t d_first, uint32_t d_stride, uint32_t nd, uint64_t *out,
+                                void *stream);
+
 /* Message of the last failing call on this thread. */
 const char *marlnav_last_error(void);
 

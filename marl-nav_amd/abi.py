@@ -65,7 +65,7 @@ EXPORTS = ("marlnav_step", "marlnav_observe", "marlnav_reinit_all", "marlnav_for
            "marlnav_returns_work_size", "marlnav_discounted_returns",
            "marlnav_last_error", "marlnav_abi_version",
            "marlnav_debug_force_family", "marlnav_debug_last_family",
-           "marlnav_debug_acos_range")
+           "marlnav_debug_acos_range", "marlnav_debug_fastdiv_check")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmarlnav.so")
@@ -104,6 +104,10 @@ def _declare(lib):
     if hasattr(lib, "marlnav_debug_acos_range"):  # (absent from A/B builds of older revisions)
         lib.marlnav_debug_acos_range.argtypes = [c.c_uint32, c.c_int64, c.c_void_p, c.c_void_p]
         lib.marlnav_debug_acos_range.restype = c.c_int
+    if hasattr(lib, "marlnav_debug_fastdiv_check"):
+        lib.marlnav_debug_fastdiv_check.argtypes = [c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p,
+                                                    c.c_void_p]
+        lib.marlnav_debug_fastdiv_check.restype = c.c_int
     return lib
 
 

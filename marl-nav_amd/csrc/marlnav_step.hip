@@ -126,6 +126,45 @@ __global__ void acos_range_kernel(uint32_t first, int64_t n, float *__restrict__
     if (i < n) out[i] = acos_k(__uint_as_float(first + (uint32_t)i));
 }
 
+// marlnav_debug_fastdiv_check: the step kernels' short division sequences
+// (div2_fast, div_c with make_divc, recip_fast; device_math.h) against IEEE
+// division, for the d significands d_first + k * d_stride (k < gridDim.x) in
+// [1, 2) and EVERY x significand in [1, 2) - the pairs that decide every
+// guarded case (the sequences are scale- and sign-invariant inside the
+// guards). out[0..2] += mismatching (x, d) pairs of div2_fast, div_c, and
+// mismatching d of recip_fast.
+__global__ void __launch_bounds__(256) fastdiv_check_kernel(uint32_t d_first, uint32_t d_stride,
+                                                            unsigned long long *__restrict__ out)
+{
+    const uint32_t dm = (d_first + blockIdx.x * d_stride) & 0x7FFFFFu;
+    const float d = __uint_as_float(0x3f800000u | dm);
+    bool ok = true;
+    const DivC dc = make_divc(d, ok);
+    unsigned long long b_div2 = 0, b_divc = 0;
+    if (threadIdx.x == 0 &&
+        __float_as_uint(recip_fast(d, ok)) != __float_as_uint(1.0f / d))
+        atomicAdd(&out[2], 1ull);
+    for (uint32_t xm = threadIdx.x; xm < (1u << 23); xm += 2 * blockDim.x) {
+        const float x = __uint_as_float(0x3f800000u | xm);
+        const float y = __uint_as_float(0x3f800000u | (xm + blockDim.x));
+        float qx, qy;
+        div2_fast(x, y, d, &qx, &qy, ok);
+        b_div2 += (__float_as_uint(qx) != __float_as_uint(x / d)) +
+                  (__float_as_uint(qy) != __float_as_uint(y / d));
+        b_divc += __float_as_uint(div_c(x, dc, ok)) != __float_as_uint(x / d);
+        b_divc += __float_as_uint(div_c(y, dc, ok)) != __float_as_uint(y / d);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        b_div2 += __shfl_xor(b_div2, o);
+        b_divc += __shfl_xor(b_divc, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (b_div2) atomicAdd(&out[0], b_div2);
+        if (b_divc) atomicAdd(&out[1], b_divc);
+    }
+    if (!ok && threadIdx.x == 0) atomicAdd(&out[2], 1ull << 32);  // (a guard refused: never here)
+}
+
 __global__ void counters_total_kernel(const uint64_t *__restrict__ c, int64_t slots,
                                       uint64_t *out3)
 {
@@ -464,6 +503,17 @@ int marlnav_debug_acos_range(uint32_t first, int64_t n, float *out, void *stream
                        (hipStream_t)stream, first, n, out);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(MARLNAV_ELAUNCH, "acos range: %s", hipGetErrorString(e));
+}
+
+int marlnav_debug_fastdiv_check(uint32_t d_first, uint32_t d_stride, uint32_t nd, uint64_t *out,
+                                void *stream)
+{
+    if (nd > 0 && !out) return fail(MARLNAV_EINVAL, "fastdiv check: out NULL");
+    if (nd == 0) return 0;
+    hipLaunchKernelGGL(fastdiv_check_kernel, dim3(nd), dim3(256), 0, (hipStream_t)stream, d_first,
+                       d_stride, reinterpret_cast<unsigned long long *>(out));
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(MARLNAV_ELAUNCH, "fastdiv check: %s", hipGetErrorString(e));
 }
 
 const char *marlnav_last_error(void) { return g_err; }

@@ -1378,6 +1378,28 @@ def test_kernel_acos_equals_oracle_restatement(pkg, first, n):
                            f"{first + int(bad[0]):#010x}: {got[bad[0]]!r} vs {exp[bad[0]]!r}")
 
 
+@pytest.mark.parametrize("d_first,d_stride,nd", [
+    (0, 127, 65536),             # 1/128 of the divisor significands, spread over [1, 2)
+    (0x7FFFFF - 255, 1, 256),    # the last 256, up to the all-ones significand
+    (0, 1, 256),                 # 1.0 and its neighbours
+])
+def test_fast_division_sequences_exact(pkg, d_first, d_stride, nd):
+    """The kernels' short division sequences (div2_fast / div_c: one Newton
+    step and ONE residual correction; recip_fast: the Newton step alone)
+    against IEEE division, through marlnav_debug_fastdiv_check, for every
+    dividend significand of each sampled divisor: zero mismatches. Inside the
+    guards the sequences are scale- and sign-invariant, so significand pairs
+    decide every case; scripts/probes/div_exhaustive.hip checks all 2^46
+    (profiles/r05_div_exhaustive.txt)."""
+    lib = pkg.abi.load_library()
+    out = torch.zeros(3, dtype=torch.int64, device=DEV)  # (65536 x 2^23 pairs: ~0.3 s)
+    assert lib.marlnav_debug_fastdiv_check(d_first, d_stride, nd, out.data_ptr(), None) == 0
+    got = [int(v) for v in np_(out)]
+    assert got == [0, 0, 0], (f"mismatches over {nd} divisors x 2^23 dividends: quotients {got[0]}, "
+                              f"parameter divisions {got[1]}, reciprocals {got[2] & 0xFFFFFFFF}, "
+                              f"guard refusals {got[2] >> 32}")
+
+
 def test_kernel_acos_strided_sample(pkg):
     """Every 997th fp32 of [-1, 1] through the kernels' acos vs the oracle's,
     evaluated in chunks of 2^24 consecutive patterns (64 MB of device output
