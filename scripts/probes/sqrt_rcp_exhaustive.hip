@@ -1,6 +1,6 @@
 // Exhaustive check, on the GPU, of two shortcuts in the pair distance and the
 // normalisation that follows it (device_math.h sqrt_fast / div2_fast), over
-// EVERY fp32 x in [2^-78, 2^96) (x = dx^2 + dy^2, the sqrt_fast guard range):
+// EVERY fp32 x in [2^-96, 2^96) (x = dx^2 + dy^2, the sqrt_fast guard range):
 //   S0: sqrt_fast as shipped: y = rsq(x), s = x y, h = y / 2, e = x - s s,
 //       max(s + e h, 0)                                     == sqrtf(x)
 //   S1: the halving moved into the FMA's output modifier: e2 = (x - s s) / 2
@@ -63,7 +63,7 @@ __global__ void run(uint32_t lo, uint32_t n, unsigned long long *cnt, uint32_t *
 
 int main()
 {
-    const uint32_t lo = (uint32_t)(127 - 78) << 23, hi = (uint32_t)(127 + 96) << 23;
+    const uint32_t lo = (uint32_t)(127 - 96) << 23, hi = (uint32_t)(127 + 96) << 23;
     unsigned long long *cnt;
     uint32_t *ex;
     hipMalloc(&cnt, 5 * sizeof(unsigned long long));
@@ -75,7 +75,7 @@ int main()
     uint32_t e[48];
     hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost);
     hipMemcpy(e, ex, sizeof e, hipMemcpyDeviceToHost);
-    printf("x in [2^-78, 2^96): %u values; S0 (shipped sqrt_fast) fails %llu, S1 (div:2 FMA) fails %llu, "
+    printf("x in [2^-96, 2^96): %u values; S0 (shipped sqrt_fast) fails %llu, S1 (div:2 FMA) fails %llu, "
            "R1 (rsq-started reciprocal) fails %llu, R2 (two Newton steps) fails %llu\n", hi - lo, h[0], h[1],
            h[2], h[4]);
     for (unsigned long long k = 0; k < (h[3] < 16 ? h[3] : 16); ++k)
