@@ -618,7 +618,21 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         sn_in = b.step_num[e0 + lane];
         term_in = b.terminates[e0 + lane];
     }
-    const MarlnavParams pr = load_params(K);
+    MarlnavParams pr = load_params(K);
+    if constexpr (MARLNAV_OWN_VPIN == 2 || (MARLNAV_OWN_VPIN && kSplitOwn<A, O, LPR, OWN>)) {
+        // the pair loops' and reward terms' parameters held in VGPRs: the
+        // own-wave instantiation otherwise runs out of SGPRs (59 spilled to
+        // VGPR lanes, reloaded in the observation's hot blocks; 20 left, in
+        // cold blocks). Every split kernel (MARLNAV_OWN_VPIN 2): 4096x16x32
+        // 11.23 -> 11.30 us, not taken
+        const auto pin = [](float &x) { asm volatile("" : "+v"(x)); };
+        pin(pr.ob_risk_dist); pin(pr.ob_coll_dist); pin(pr.ag_risk_dist); pin(pr.ag_coll_dist);
+        pin(pr.agents_min_d); pin(pr.agents_max_d); pin(pr.ideal_dist); pin(pr.bond_sharpness);
+        pin(pr.cap_distance); pin(pr.max_angle_diff); pin(pr.max_at_prop_d); pin(pr.init_dist);
+        pin(pr.target_factor); pin(pr.heading_factor); pin(pr.distance_factor);
+        pin(pr.soft_factor); pin(pr.bond_factor); pin(pr.risk_factor); pin(pr.target_radius);
+        pin(pr.trunc_after);
+    }
     const bool wt = (pr.flags & kWriteThroughFlag) != 0;  // written-through outputs
     float *const pre = lds + kWavesPerBlock * SP::FLOATS + SP::PRE;
     // the workgroup's live waves (the waves past the last tile have exited)

@@ -80,6 +80,12 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_LATE_PTRS
 #define MARLNAV_LATE_PTRS 1  // 0: block kernel output pointers held from the entry (A/B builds)
 #endif
+#ifndef MARLNAV_SPLIT_OWN_MAX
+#define MARLNAV_SPLIT_OWN_MAX 2048  // the own-wave instantiation for A16/O32 grids of at most this many envs
+#endif
+#ifndef MARLNAV_OWN_VPIN
+#define MARLNAV_OWN_VPIN 1  // own-wave split instantiation's parameters in VGPRs (0: off; 2: every split kernel, A/B)
+#endif
 #ifndef MARLNAV_SPLIT_EARLY
 #define MARLNAV_SPLIT_EARLY 1  // 0: own-wave split tiles stored after the per-env phase (A/B builds;
                                // early: 8.38 vs 8.48 us at 2048x16x32, profiles/r05_ab_early.txt)

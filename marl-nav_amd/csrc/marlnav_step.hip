@@ -293,10 +293,12 @@ constexpr int64_t kSplitTinyWaves = 256;
 // most two waves per SIMD (one env per wave): same box, graph replay,
 // steady (profiles/r05_ab_tail_own2.txt, r05_ab_tail_ablate.txt): 512x16x32
 // 7.98 -> 7.44 us, 1024x16x32 8.28 -> 7.58, 2048x16x32 9.27 -> 8.48;
-// 4096x16x32 (four waves per SIMD) 11.59-11.62 -> 11.65-11.67. Since the
-// one-correction division its code generation lost that margin at 2048
-// envs (own 9.93 vs 9.15 us; 1024: 7.93 vs 8.13; profiles/r05_ab_own_regress.txt)
-constexpr int64_t kSplitOwnMaxEnvs = 1024;
+// 4096x16x32 (four waves per SIMD) 11.59-11.62 -> 11.65-11.67. With the
+// one-correction division its register allocation spilled SGPRs into the
+// observation's hot blocks (2048: 9.96 us); with its parameters held in
+// VGPRs (MARLNAV_OWN_VPIN, kernel_split.h) 8.24 us, 1024 7.44, 512 7.28
+// against 9.14 / 7.93 / 7.78 for the default kernel (profiles/r05_ab_vpin.txt)
+constexpr int64_t kSplitOwnMaxEnvs = MARLNAV_SPLIT_OWN_MAX;
 #undef MARLNAV_SPLIT_VARIANT
 
 // one-lane-per-row grids below kSplitBelowWaves * (pairs per row / 6) waves
