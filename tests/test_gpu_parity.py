@@ -190,7 +190,7 @@ class _nullctx:
                                             (12000 + 7, 3, 3, 9, 4), (20480, 3, 8, 5, 2),
                                             (1021, 16, 32, 6, 3), (1000 + 3, 3, 8, 8, 3),
                                             (16384, 3, 3, 8, 3), (32768 + 5, 3, 3, 6, 4),
-                                            (8192 + 3, 3, 3, 6, 2)])
+                                            (8192 + 3, 3, 3, 6, 2), (2048, 16, 32, 4, 2)])
 def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
     """Native (Philox) re-init mode, many steps, random actions, short
     episodes (ep = 2, 4: whole tiles finish at once, re-observed in several
@@ -198,7 +198,9 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
     split-kernel cases end on a workgroup with fewer live waves (1021 = 255*4
     + 1 one-env waves) and a partial tile (1003 envs, two per LPR-8 wave).
     16384 (configs[4]'s per-GPU shape), 8195 (ragged last block) and 32773
-    envs at 3-step and shorter episodes: many finished envs every step."""
+    envs at 3-step and shorter episodes: many finished envs every step.
+    512, 1021 and 2048 x 16 x 32 run the split kernel's own-wave
+    instantiation (finished envs re-initialised by their own wave)."""
     g = torch.Generator().manual_seed(P + A + O)
     env = make_env(pkg, P, A, O, episode_len=ep, seed=99,
                    factors=dict(risk_factor=3., distance_factor=7.))
