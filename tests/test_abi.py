@@ -85,6 +85,13 @@ def test_validation_errors_are_loud(pkg):
     assert lib.marlnav_counter_slots(ctypes.byref(d)) == 4
     d.num_parallel = 65536
     assert lib.marlnav_counter_slots(ctypes.byref(d)) == 3280
+    # the testing hooks check their arguments before any launch
+    assert lib.marlnav_debug_acos_range(0, -1, None, None) == -1
+    assert b"acos range" in lib.marlnav_last_error()
+    assert lib.marlnav_debug_acos_range(0, 0, None, None) == 0
+    assert lib.marlnav_debug_fastdiv_check(0, 1, 4, None, None) == -1
+    assert b"fastdiv check" in lib.marlnav_last_error()
+    assert lib.marlnav_debug_fastdiv_check(0, 1, 0, None, None) == 0
 
 
 def test_missing_library_is_an_error(pkg, tmp_path):
