@@ -302,8 +302,11 @@ constexpr int64_t kSplitOwnMaxEnvs = MARLNAV_SPLIT_OWN_MAX;
 #undef MARLNAV_SPLIT_VARIANT
 
 // one-lane-per-row grids below kSplitBelowWaves * (pairs per row / 6) waves
-// leave most SIMDs idle (measured: 16384x3x8 split faster, 16384x3x3 not)
-constexpr int64_t kSplitBelowWaves = 512;
+// leave most SIMDs idle. A3/O8 (11 pairs): split below 587 wave tiles, i.e.
+// about 11700 envs (round 5, graph replay, scripts/diag/family_ab.py,
+// profiles/r05_family_ab.txt: 10240x3x8 split 6.17 vs block 6.46 us, 12288
+// 6.67 vs 6.50, 16384 7.35 vs 6.51; round 2 had split faster at 16384)
+constexpr int64_t kSplitBelowWaves = 320;
 // ... except that with at most 6 pairs per row (A3/O3) the env-block kernel is
 // faster from one full block of 64 envs on (graph replay, round 2, with
 // kernarg preload: 64x3x3 4.20 vs 4.28 us, 1024x3x3 5.23 vs 5.37, 4096x3x3
