@@ -19,7 +19,7 @@ for P, A, O in shapes:
     g = torch.Generator(device=dev).manual_seed(1234)
     acts = [(torch.rand(P, A, 2, generator=g, device=dev) - 0.5) for _ in range(8)]
     res = []
-    for fam in (0, 1, 2):
+    for fam in tuple(int(f) for f in os.environ.get("FAMILIES", "0,1,2").split(",")):
         env = bench.make_env(pkg, P, A, O, dev, 0, seed=20251004)
         lib = env._lib
         prev = lib.marlnav_debug_force_family(fam)
