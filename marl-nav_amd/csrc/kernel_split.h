@@ -569,6 +569,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS
     int stamp_nfin = 0;
+    int stamp_fast = 0;  // (the wave took the short pair math: bit 8 of the nfin slot)
 #endif
 #if MARLNAV_STAMPS
     unsigned long long t_entry;
@@ -777,6 +778,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                              tile_coords_ok<EPW * O * 2, EPW * 2>(wl + SP::OB, wl + SP::TG, lane);
             fast = ne == EPW && __ballot(!cok) == 0ull;
         }
+#if MARLNAV_STAMPS
+        stamp_fast = fast ? 1 : 0;
+#endif
         bool unused = true;
         SplitTerms t;
         if constexpr (kSplitOwn<A, O, LPR, OWN> && !OBS_ONLY) {
@@ -1026,6 +1030,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     };
 
     bool stored = false;  // (the tile went out before the per-env barrier)
+    bool tail_wg = false;  // (AB 1 << 19, timing only: a workgroup with finished envs skips its stores)
     if (!OBS_ONLY) {
         wave_sync();
         // ---- per-env reductions, terminal logic, masked re-init (env e,
@@ -1186,6 +1191,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             // (kSplitOwn with the template: every finished env was re-initialised
             // and re-observed by its own wave before the per-env barrier)
             const bool own_done = kSplitOwn<A, O, LPR, OWN> && tpl_on;
+            if ((MARLNAV_AB & (1 << 19)) && list.total()) tail_wg = true;
             if (const int nfin = ((MARLNAV_AB & 1) || own_done) ? 0 : list.total()) {  // (AB 1: timing only)
                 KArgsK *kl = kargs_late<kHotKargsOff>();
                 const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
@@ -1262,6 +1268,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     // ---- stream the tile out (obs rows and states from LDS)
     wave_sync();
     if (MARLNAV_AB & 2) return;  // (AB 2: timing only - no store)
+    if ((MARLNAV_AB & (1 << 19)) && tail_wg) return;
     if (!stored) store_tile();
     STAMP(6);
     if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
@@ -1282,7 +1289,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         *STAMP_PTR((size_t)gw * 24 + 16) = t_entry;
         *STAMP_PTR((size_t)gw * 24 + 17) = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
         *STAMP_PTR((size_t)gw * 24 + 18) = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
-        *STAMP_PTR((size_t)gw * 24 + 19) = (unsigned)stamp_nfin;
+        *STAMP_PTR((size_t)gw * 24 + 19) = (unsigned)stamp_nfin | ((unsigned)stamp_fast << 8);
     }
 #endif
 }

@@ -46,6 +46,8 @@ def main():
             raw = buf.view(nb, 24).cpu().numpy().astype(np.int64)
             gidx = np.nonzero(raw[:, 0] > 0)[0]  # stamps slot = global wave index
             raw = raw[raw[:, 0] > 0]  # waves past the last tile record nothing
+            fastw = (raw[:, 19] >> 8) & 1  # (split kernel: the wave took the short pair math)
+            raw[:, 19] &= 0xff
             st = raw[:, :16].reshape(-1, 8, 2)
             entry = raw[:, 16] * 10.0 / 1e3
             rt = st[:, :, 0] * 10.0 / 1e3  # 100 MHz ticks -> us
@@ -103,6 +105,9 @@ def main():
               "with_finished_envs": int((raw[slow, 19] > 0).sum())})
         # waves that re-observed finished envs vs the rest: do they set the end?
         reo = raw[:, 19] > 0  # tiles with a finished env (re-init + re-observe)
+        if fastw.any():
+            print(cfg, "short pair math: with finished envs", f"{fastw[reo].mean():.3f}",
+                  "without", f"{fastw[~reo].mean():.3f}", flush=True)
         fin_t = rt[:, 7] - t0
         for name, m in (("with_reobs", reo), ("without", ~reo)):
             if m.any():
