@@ -1187,6 +1187,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             const FlatFinList list{bslot, bcnt[0]};
 #if MARLNAV_STAMPS
             stamp_nfin = list.total();
+            for (int f = 0; f < list.total(); ++f)  // (bit 9: this wave's own env finished)
+                if (list[f] / EPW == wib) stamp_nfin |= 1 << 9;
 #endif
             // (kSplitOwn with the template: every finished env was re-initialised
             // and re-observed by its own wave before the per-env barrier)

@@ -47,6 +47,7 @@ def main():
             gidx = np.nonzero(raw[:, 0] > 0)[0]  # stamps slot = global wave index
             raw = raw[raw[:, 0] > 0]  # waves past the last tile record nothing
             fastw = (raw[:, 19] >> 8) & 1  # (split kernel: the wave took the short pair math)
+            ownf = (raw[:, 19] >> 9) & 1   # (split kernel: the wave's own env finished)
             raw[:, 19] &= 0xff
             st = raw[:, :16].reshape(-1, 8, 2)
             entry = raw[:, 16] * 10.0 / 1e3
@@ -108,6 +109,20 @@ def main():
         if fastw.any():
             print(cfg, "short pair math: with finished envs", f"{fastw[reo].mean():.3f}",
                   "without", f"{fastw[~reo].mean():.3f}", flush=True)
+        print(cfg, "clock GHz median: with finished envs", round(float(np.median(clk[reo])), 3),
+              "without", round(float(np.median(clk[~reo])), 3),
+              "| entry us median: with", round(float(np.median(entry[reo] - t0)), 2),
+              "without", round(float(np.median(entry[~reo] - t0)), 2),
+              "| observed-phase cycles median: with",
+              int(np.median(cy[reo, 3] - cy[reo, 2])), "without", int(np.median(cy[~reo, 3] - cy[~reo, 2])),
+              flush=True)
+        if ownf.any():
+            om = reo & (ownf == 1)
+            nm = reo & (ownf == 0)
+            print(cfg, "observed-phase cycles median in workgroups with finished envs: the finished env's wave",
+                  int(np.median(cy[om, 3] - cy[om, 2])), f"(n={int(om.sum())})", "its other waves",
+                  int(np.median(cy[nm, 3] - cy[nm, 2])) if nm.any() else None, f"(n={int(nm.sum())})",
+                  flush=True)
         fin_t = rt[:, 7] - t0
         for name, m in (("with_reobs", reo), ("without", ~reo)):
             if m.any():
