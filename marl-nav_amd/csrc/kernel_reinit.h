@@ -429,6 +429,88 @@ __device__ __forceinline__ void reinit_reobs_tpl(KArgsK *kl, const Envs &ev, con
     const float rx = kl->p.obs_range_x, mx = kl->p.obs_mean_x;
     const float ry = kl->p.obs_range_y, my = kl->p.obs_mean_y;
     const int j = tid % O, ag0 = tid / O;
+    if constexpr (MARLNAV_TPL_LOADS_FIRST && A * A <= NT && 5 * A + 2 <= NT) {
+        // (A/B) every LDS read of the pass first, then the Philox block and
+        // the pair math, then every write: one LDS round trip in front of
+        // the chain instead of one per step
+        constexpr int KA = (A + agd - 1) / agd;
+        for (int fe = 0; fe < nfin; ++fe) {
+            const int c = list[fe];
+            const int64_t e = ev.env(c);
+            const bool has_t = tid < A * A;
+            const float2 tv = tpl[has_t ? tid : 0];
+            const int k2 = tid;
+            const bool has_b = k2 < 5 * A + 2;
+            const bool btg = k2 >= 5 * A;
+            float *bd = btg ? ev.targ(c) + (k2 - 5 * A) : ev.state(c) + (has_b ? k2 : 0);
+            const float bold = *bd, bform = form[has_b ? k2 : 0];
+            const float *oo = ev.obst(c) + 2 * j;
+            const float oox = oo[0], ooy = oo[1];
+            float so[KA][4], sf[KA][4];
+#pragma unroll
+            for (int k = 0; k < KA; ++k) {
+                const int ag = ag0 + k * agd;
+                const int agc = ag < A ? ag : 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    so[k][q] = ev.state(c)[5 * agc + q];
+                    sf[k][q] = form[5 * agc + q];
+                }
+            }
+            float v[2];
+            native_obst_draw(seed, sidx, (uint64_t)(eoff + e), j, rx, mx, ry, my, v);
+            const float px = blend_in(oox, v[0]);
+            const float py = blend_in(ooy, v[1]);
+            float dd[KA], aa[KA];
+#pragma unroll
+            for (int k = 0; k < KA; ++k) {
+                const bool on = ag0 + k * agd < A;
+                const float ox = blend_in(so[k][0], sf[k][0]), oy = blend_in(so[k][1], sf[k][1]);
+                const float dx = blend_in(so[k][2], sf[k][2]), dy = blend_in(so[k][3], sf[k][3]);
+                const bool cok = coord_ok(ox) && coord_ok(oy) && coord_ok(px) && coord_ok(py);
+                bool unused = true;
+                if (__ballot(on && !cok) == 0ull) {
+                    dd[k] = pair_dist<true>(ox, oy, px, py, unused);
+                    aa[k] = pair_angle<true>(ox, oy, px, py, dx, dy, dd[k], cap, unused);
+                } else {
+                    dd[k] = pair_dist<false>(ox, oy, px, py, unused);
+                    aa[k] = pair_angle<false>(ox, oy, px, py, dx, dy, dd[k], cap, unused);
+                }
+            }
+            // writes: template pair, blend, the pairs, the obstacle
+            if (has_t) {
+                const int ag = tid / A, m = tid - ag * A;
+                const int sa = m == 0 ? 0 : 2 + 2 * O + (m - 1);
+                const int sd = m == 0 ? 1 : 2 + 2 * O + (A - 1) + (m - 1);
+                float *o = ev.row(c, ag);
+                o[sa] = tv.y < cap ? 0.0f : tv.x;  // the cap (environment.py:172-177)
+                o[sd] = tv.y;
+            }
+            if (has_b) {
+                const float vb = blend_in(bold, bform);
+                *bd = vb;
+                if (btg) out_el(gtg, 2 * e + (k2 - 5 * A), vb);
+                if ((btg || k2 % 5 < 4) && __float_as_uint(vb) != __float_as_uint(bform)) *unclean = 1;
+            }
+#pragma unroll
+            for (int k = 0; k < KA; ++k) {
+                const int ag = ag0 + k * agd;
+                if (ag < A) {
+                    float *o = ev.row(c, ag);
+                    o[2 + j] = aa[k];
+                    o[2 + O + j] = dd[k];
+                }
+            }
+            if (ag0 == 0) {
+                float *ow = ev.obst(c) + 2 * j;
+                ow[0] = px;
+                ow[1] = py;
+                out_el(gob, e * O * 2 + 2 * j, px);
+                out_el(gob, e * O * 2 + 2 * j + 1, py);
+            }
+        }
+        return;
+    }
     for (int fe = 0; fe < nfin; ++fe) {
         const int c = list[fe];
         const int64_t e = ev.env(c);
