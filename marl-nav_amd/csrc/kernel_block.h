@@ -190,14 +190,18 @@ constexpr bool kBlockEarlyOut = MARLNAV_EARLY_OUT < 0 ? O >= 8 : MARLNAV_EARLY_O
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
 // re-init; none in most blocks) | rows and states stream out of LDS.
-template <int A, int O, bool OBS_ONLY, bool NOISY>
-__global__ void __launch_bounds__(64 * A)
+template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false>
+__global__ void __launch_bounds__(64 * (A + HELP))
     block_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
                  const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
                  int64_t h_P, KArgs k)
 {
     using BP = BlockPlan<A, O>;
+    // NT: the agent waves' threads, over which every work loop is spread
+    // (HELP: one more wave, w == A, draws the fresh obstacles and otherwise
+    // only meets the barriers)
     constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
+    static_assert(!HELP || (!OBS_ONLY && !NOISY), "the draw wave serves the native re-init step");
     (void)k;  // read through kargs_late<kHotKargsOff>()
     extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS
@@ -208,8 +212,9 @@ __global__ void __launch_bounds__(64 * A)
     const int tid = (int)threadIdx.x;
     const unsigned lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // agent of this wave
+    const bool hw = HELP && w == A;  // the draw wave (no agent)
     const int64_t blk = blockIdx.x;
-    const int64_t gw = blk * A + w;  // stamps slot
+    const int64_t gw = blk * (A + HELP) + w;  // stamps slot
     KArgsK *K = kargs_late<kHotKargsOff>();
     const int64_t P = h_P;
     // launch_block's grid is exactly ntiles blocks: no exit test. The staging
@@ -232,8 +237,8 @@ __global__ void __launch_bounds__(64 * A)
     // them alone (vmcnt = the span instructions it issued after them) and
     // evaluates the heading's sin/cos while the spans are still in flight,
     // not after the stage barrier
-    float *actw = lds + BP::ACTW + 2 * E * w;  // x at [l], y at [E + l]
-    if (!OBS_ONLY && full) {
+    float *actw = lds + BP::ACTW + 2 * E * (hw ? 0 : w);  // x at [l], y at [E + l]
+    if (!OBS_ONLY && full && !hw) {
         const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
         __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
         __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
@@ -253,7 +258,7 @@ __global__ void __launch_bounds__(64 * A)
             if (b.formation)
                 block_glds<BS::NB[5]>(BS::K[5], A, w, b.formation, lds + BP::FORM, lane);
         }
-    } else {
+    } else if (!hw) {
         const int nr = ne * A;
         block_copy(b.states + e0 * (A * 5), st, nr * 5, tid, NT);
         if (!OBS_ONLY && (int)lane < ne) {  // (each lane its own slots: no barrier)
@@ -279,7 +284,25 @@ __global__ void __launch_bounds__(64 * A)
     // the stage phase more than they save there, 131072x3x8 18.4 -> 19.0 us
     // with the round-4 Philox4x32)
     constexpr bool kPre = E * O <= NT;
-    if (kPre && overlap && !(MARLNAV_AB & 256)) {  // (AB 256: timing only, no draws)
+    if constexpr (HELP) {
+        // the draw wave: the same draws, O per lane (env `lane`), on the
+        // SIMD the agent waves leave idle
+        if (hw && overlap && !(MARLNAV_AB & 256) && (int)lane < ne) {
+            KArgsK *kl = kargs_late<kHotKargsOff>();
+            const uint64_t sidx = kl->a.step_idx, g = (uint64_t)(kl->a.env_offset + e0) + lane;
+            float *pre = lds + BP::FRESH;
+            float v[O][2];
+#pragma unroll
+            for (int j = 0; j < O; ++j)
+                native_obst_draw(pr.seed, sidx, g, j, pr.obs_range_x, pr.obs_mean_x, pr.obs_range_y,
+                                 pr.obs_mean_y, v[j]);
+#pragma unroll
+            for (int j = 0; j < O; ++j) {
+                pre[(2 * j) * E + lane] = v[j][0];
+                pre[(2 * j + 1) * E + lane] = v[j][1];
+            }
+        }
+    } else if (kPre && overlap && !(MARLNAV_AB & 256)) {  // (AB 256: timing only, no draws)
         // the fresh obstacles of every env of the block (its Philox draws
         // depend only on seed, step and env id), drawn while the staging
         // loads are in flight: a finished env's re-init then reads them
@@ -306,7 +329,7 @@ __global__ void __launch_bounds__(64 * A)
     // the heading's sin/cos (environment.py:113-115, 131-137), under the
     // remaining staging latency
     float sn = 0.0f, c = 1.0f, a1 = 0.0f;
-    if (!OBS_ONLY) {
+    if (!OBS_ONLY && !hw) {
         if (full) {
             // span instructions this wave issued after its two action loads
             // (BlockSpans: the same table as the issue sites above)
@@ -326,8 +349,8 @@ __global__ void __launch_bounds__(64 * A)
         sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
     }
     const int l = (int)lane;  // env of this lane within the block
-    const int r = l * A + w;  // row of this lane
-    const bool row_on = l < ne;
+    const int r = l * A + (hw ? 0 : w);  // row of this lane (the draw wave has none)
+    const bool row_on = l < ne && !hw;
     const int nrow = ne * A;
     int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
     if (tid == 0) *bad_word = 0;
@@ -343,7 +366,7 @@ __global__ void __launch_bounds__(64 * A)
     // (below); read before the move writes LDS, so the reads overlap it
     // (a partial last block takes the IEEE path without checking)
     CoordRange crange;
-    if (full) {
+    if (full && !hw) {
         constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
         static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
 #pragma unroll
@@ -384,7 +407,7 @@ __global__ void __launch_bounds__(64 * A)
     // reciprocal division (equal to IEEE there) when every coordinate of the
     // block (obstacles and targets above, moved agents here) passes coord_ok,
     // IEEE otherwise
-    if (full) {
+    if (full && !hw) {
         crange.add(ox);
         crange.add(oy);
         // one word for the block, written only by waves that found one (all
@@ -546,7 +569,7 @@ __global__ void __launch_bounds__(64 * A)
             }
             STAMPX(2);  // (wave 0: list, counts and counters done)
             if (MARLNAV_ENV_PRIO) __builtin_amdgcn_s_setprio(0);
-        } else if (overlap) {
+        } else if (overlap && !hw) {
             // ---- waves 1..A-1, while wave 0 runs the per-env phase: the
             // finished set from the inputs wave 0 uses (red flags, step_num,
             // terminates), then the native re-init (:104) and re-observation
@@ -589,15 +612,17 @@ __global__ void __launch_bounds__(64 * A)
             // ---- reference-RNG / noisy re-init (:104; noisy: done above by
             // wave 0) and observations of the re-initialised envs (:105)
             if (!NOISY) {
-                reinit_block<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, list, nfin, tid, NT);
+                if (!hw) reinit_block<A, O>(kargs_late<kHotKargsOff>(), ev, lds + BP::FORM, list, nfin, tid, NT);
                 __syncthreads();
             }
-            reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, NT);
+            if (!hw) reobs_block<A, O>(ev, list, nfin, pr.cap_distance, tid, NT);
             __syncthreads();
         }
     }
     STAMP(5);
-    if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
+    if (hw) {  // (the draw wave stores nothing; it meets the norm path's barrier)
+        if (!OBS_ONLY && !(full && !norm) && !(full && NT % D == 0) && norm) __syncthreads();
+    } else if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
         if (!(MARLNAV_AB & 2) && !early)
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)),
                                                st, tid, wt);  // (E = 64: whole 16-byte pieces)

@@ -83,6 +83,9 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_SPLIT_OWN_MAX
 #define MARLNAV_SPLIT_OWN_MAX 2048  // the own-wave instantiation for A16/O32 grids of at most this many envs
 #endif
+#ifndef MARLNAV_DRAW_WAVE
+#define MARLNAV_DRAW_WAVE 1  // 0: no draw-wave block instantiation (A/B builds)
+#endif
 #ifndef MARLNAV_TPL_LOADS_FIRST
 #define MARLNAV_TPL_LOADS_FIRST 1  // 0: the template re-init pass interleaves its LDS reads and writes (r05 A/B)
 #endif

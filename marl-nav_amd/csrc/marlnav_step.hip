@@ -365,15 +365,28 @@ int launch_split(const SplitVariant &v, BlockFn fn, const StepArgs &args, const 
 }
 
 // env-block kernels (block_kernel) for these shapes
+constexpr int64_t kDrawWaveMaxBlocks = 256;
 struct BlockVariant {
     int A, O;
     BlockFn step, obs, noisy;
     size_t lds;
+    BlockFn step_draw;  // (or null) the step with a draw wave: grids of at most one block per CU
 };
+
+// The draw-wave instantiation (block_kernel HELP): the native re-init's
+// fresh-obstacle draws move from the agent waves' stage to a fourth wave on
+// the SIMD a one-block-per-CU grid leaves idle (O draws per lane: O <= 3)
+template <int A, int O>
+constexpr BlockFn block_draw_fn()
+{
+    if constexpr (O <= 3 && MARLNAV_DRAW_WAVE) return block_kernel<A, O, false, false, true>;
+    else return nullptr;
+}
 
 #define MARLNAV_BLOCK_VARIANT(A, O)                                                    \
     {A, O, block_kernel<A, O, false, false>, block_kernel<A, O, true, false>,          \
-     block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4}
+     block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4,             \
+     block_draw_fn<A, O>()}
 const BlockVariant kBlockVariants[] = {
     MARLNAV_BLOCK_VARIANT(3, 3),
     MARLNAV_BLOCK_VARIANT(3, 8),
@@ -399,7 +412,7 @@ const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers 
 }
 
 int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const MarlnavParams &pr,
-                 void *stream, const char *what)
+                 void *stream, const char *what, int waves = 0)
 {
     KArgs ka;
     ka.a = args;
@@ -415,7 +428,7 @@ int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const 
     void *kargs[] = {&h_states, &h_actions, &h_obstacles, &h_target, &h_step_num, &h_terminates,
                      &h_P, &ka};
     hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)ka.a.ntiles),
-                                   dim3(64 * v.A), kargs, v.lds, (hipStream_t)stream);
+                                   dim3(64 * (waves ? waves : v.A)), kargs, v.lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
     return 0;
@@ -601,6 +614,10 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
     if (family_allowed(MARLNAV_FAMILY_BLOCK))
         if (const BlockVariant *v = select_block(d, args.b, false)) {
             g_last_family = MARLNAV_FAMILY_BLOCK;
+            // one block per CU (MI355X: 256 CUs) leaves a SIMD of each CU idle
+            const int64_t nblk = (d->num_parallel + BlockPlan<3, 3>::E - 1) / BlockPlan<3, 3>::E;
+            if (!noisy && v->step_draw && nblk <= kDrawWaveMaxBlocks && !b->fresh_states)
+                return launch_block(*v, v->step_draw, args, *pr, stream, "marlnav_step", v->A + 1);
             return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }
     const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
