@@ -185,7 +185,9 @@ struct SplitPlan {
     // obstacle draws of the workgroup's EW envs, component k of obstacle j of
     // env code c at PRE + (2j + k) * EW + c (native_obst_draw, device_math.h)
     static constexpr int EW = kWavesPerBlock * EPW;
-    static constexpr int PRE = (FTP + (kSplitTpl<A, O> ? NCP : 0) + 3) & ~3;
+    // (kSplitSpread shapes with O <= 8: the formation alone at FTP, for the
+    // fused native re-init pass: MARLNAV_SPLIT_FORM_LDS)
+    static constexpr int PRE = (FTP + (kSplitTpl<A, O> ? NCP : (kSplitSpread<A, O> && O <= 8 && MARLNAV_SPLIT_FORM_LDS ? NF : 0)) + 3) & ~3;
     static constexpr int BLK = PRE + (kSplitSpread<A, O> && O <= 8 ? 2 * O * EW : 0);
     static_assert(EPW >= 1, "an env's rows must fit one wave");
 };
@@ -612,6 +614,21 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
         copy_span(b.obstacles + e0 * (O * 2), wl + SP::OB, ne * O * 2, (int)lane);
         copy_span(b.target + e0 * 2, wl + SP::TG, ne * 2, (int)lane);
     }
+    // kPre shapes (native re-init): the formation into FTP by LDS-DMA from
+    // wave 0 (always live), with the tile's spans (the stage wait covers it),
+    // for the fused re-init pass, whose pair items otherwise read it from
+    // global memory after the per-env barrier
+    constexpr bool kFormLds = kSplitSpread<A, O> && O <= 8 && MARLNAV_SPLIT_FORM_LDS && SP::NF <= 64;
+    bool form_lds = false;
+    if constexpr (kFormLds && !NOISY && !OBS_ONLY) {
+        KArgsK *kl = kargs_late<kHotKargsOff>();
+        const float *cfo = kl->a.b.formation;
+        form_lds = cfo && !kl->a.b.fresh_states;
+        if (form_lds && wib == 0 && lane < (unsigned)SP::NF)
+            __builtin_amdgcn_global_load_lds(cfo + lane,
+                                             (LdsVoid *)(lds + kWavesPerBlock * SP::FLOATS + SP::FTP),
+                                             4, 0, 0);
+    }
     const bool env_on = (int)lane < ne;
     float sn_in = 0.0f;
     unsigned term_in = 0u;
@@ -684,6 +701,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     constexpr int KCP = (SP::NCP + 64 * kWavesPerBlock - 1) / (64 * kWavesPerBlock);
     float cp[KCP];
     bool tpl_on = false;
+
     if constexpr (kSplitTpl<A, O> && !NOISY && !OBS_ONLY) {
         KArgsK *kl = kargs_late<kHotKargsOff>();
         const float *cfo = kl->a.b.formation, *ctp = kl->a.b.formation_obs;
@@ -1203,7 +1221,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 // fused native re-init + re-observation recomputes a Philox
                 // block per obstacle pair: only for few obstacles
                 if (!NOISY && O <= 8 && !kl->a.b.fresh_states) {
-                    reinit_reobs_native<A, O, SP::EW>(kl, ev, kl->a.b.formation, list, nfin,
+                    const float *form = form_lds ? lds + kWavesPerBlock * SP::FLOATS + SP::FTP
+                                                 : kl->a.b.formation;
+                    reinit_reobs_native<A, O, SP::EW>(kl, ev, form, list, nfin,
                                                       pr.cap_distance, tid, nt, pre);
                     __syncthreads();
                 } else if (kSplitTplPass<A, O> && tpl_on && live == kWavesPerBlock) {

@@ -83,6 +83,9 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_SPLIT_OWN_MAX
 #define MARLNAV_SPLIT_OWN_MAX 2048  // the own-wave instantiation for A16/O32 grids of at most this many envs
 #endif
+#ifndef MARLNAV_SPLIT_FORM_LDS
+#define MARLNAV_SPLIT_FORM_LDS 0  // 1: the split kernel's fused A3 re-init reads the formation from LDS (A/B)
+#endif
 #ifndef MARLNAV_DRAW_WAVE
 #define MARLNAV_DRAW_WAVE 1  // 0: no draw-wave block instantiation (A/B builds)
 #endif
