@@ -91,7 +91,8 @@ typedef struct MarlnavParams {
     float act_scale[2], act_mean[2];
     uint32_t flags;
     uint32_t reserved;
-    uint64_t seed;           /* native RNG key (Philox2x32-10) */
+    uint64_t seed;           /* native RNG seed: all 64 bits enter the Philox2x32-10
+                                keys through splitmix64 + fmix32 */
 } MarlnavParams;
 
 typedef struct MarlnavStepBuffers {

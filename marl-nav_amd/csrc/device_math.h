@@ -393,6 +393,148 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
     return bearing_of<FAST>(nx, ny, dirx, diry, dist, cap);
 }
 
+// ------------------------------------------------- packed pair math (FAST)
+// W pairs of one row per vector: the operations of pair_dist<true> +
+// pair_angle<true> (and of the device acosf, op for op as acos_device in the
+// oracle restates it) on W-wide clang vectors, which the backend lowers to
+// W/2 independent v_pk_add/mul/fma_f32 per step - two fp32 operations per
+// lane-slot where a VOP2 f32 instruction takes one, and (W >= 4) no packed
+// instruction waiting on the one before it (a dependent packed pair costs an
+// s_nop on gfx950). The per-element steps that have no packed form (v_rsq,
+// v_rcp, v_sqrt, v_max/v_med3, compares, selects) stay per element. Every
+// packed operation is the same IEEE single operation per element as its
+// scalar twin (no contraction: -ffp-contract=off, explicit fma), so the
+// results are the scalar path's bits (scripts/probes/pair_forms.hip checks
+// 2^28 random pairs, the GPU suite every kernel output against the oracle).
+// No range guard: callers are coordinate-checked (FAST) blocks and tiles.
+template <int W>
+using fv_t = float __attribute__((ext_vector_type(W)));
+typedef fv_t<2> f2_t;
+
+template <int W>
+__device__ __forceinline__ fv_t<W> pk_fma(fv_t<W> a, fv_t<W> b, fv_t<W> c)
+{
+    return __builtin_elementwise_fma(a, b, c);
+}
+
+template <int W>
+__device__ __forceinline__ fv_t<W> fvs(float x)
+{
+    return (fv_t<W>)(x);
+}
+
+// the device library's acosf (ocml), op for op (acos_device in the oracle):
+// r = |x| > 0.5 ? 0.5 - 0.5|x| : x*x; u = r P5(r); |x| <= 0.5: pi/2 - (x +
+// x u); else 2(s + s u), or pi minus that for x < 0, s = v_sqrt_f32(r)
+template <int W>
+__device__ __forceinline__ fv_t<W> acosv_dev(fv_t<W> x)
+{
+    fv_t<W> ax, r, sq, out;
+#pragma unroll
+    for (int i = 0; i < W; ++i) ax[i] = __builtin_fabsf(x[i]);
+    const fv_t<W> rt = pk_fma<W>(ax, fvs<W>(-0.5f), fvs<W>(0.5f));
+    const fv_t<W> x2 = x * x;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r[i] = ax[i] > 0.5f ? rt[i] : x2[i];
+    fv_t<W> p = pk_fma<W>(fvs<W>(__uint_as_float(0x3d1c21a7u)), r, fvs<W>(__uint_as_float(0x3c5fc5dau)));
+    p = pk_fma<W>(r, p, fvs<W>(__uint_as_float(0x3d034c3cu)));
+    p = pk_fma<W>(r, p, fvs<W>(__uint_as_float(0x3d3641b1u)));
+    p = pk_fma<W>(r, p, fvs<W>(__uint_as_float(0x3d999bc8u)));
+    p = pk_fma<W>(r, p, fvs<W>(__uint_as_float(0x3e2aaaacu)));
+    const fv_t<W> u = r * p;
+#pragma unroll
+    for (int i = 0; i < W; ++i) sq[i] = __builtin_amdgcn_sqrtf(r[i]);
+    const fv_t<W> s2 = pk_fma<W>(sq, u, sq);
+    const fv_t<W> zt = s2 + s2;
+    const fv_t<W> ztn = fvs<W>(__uint_as_float(0x40490fdbu)) - zt;
+    const fv_t<W> zs = fvs<W>(__uint_as_float(0x3fc90fdbu)) - pk_fma<W>(x, u, x);
+#pragma unroll
+    for (int i = 0; i < W; ++i) out[i] = ax[i] > 0.5f ? (x[i] < 0.0f ? ztn[i] : zt[i]) : zs[i];
+    return out;
+}
+
+// pair_dist<true> and pair_angle<true> of W pairs (px, py) of the row at
+// (ox, oy) heading (dirx, diry): the distances and the capped bearings
+template <int W>
+__device__ __forceinline__ void pairv_fast(float ox, float oy, float dirx, float diry,
+                                           fv_t<W> px, fv_t<W> py, float cap, fv_t<W> &dist,
+                                           fv_t<W> &ang)
+{
+    const fv_t<W> dx = px - fvs<W>(ox), dy = py - fvs<W>(oy);
+    const fv_t<W> q = pk_fma<W>(dy, dy, dx * dx);
+    // sqrt_fast: rsq, one FMA-residual correction, max(., 0)
+    fv_t<W> y, den, r, dot;
+#pragma unroll
+    for (int i = 0; i < W; ++i) y[i] = __builtin_amdgcn_rsqf(q[i]);
+    const fv_t<W> s = q * y, h = fvs<W>(0.5f) * y;
+    const fv_t<W> e = pk_fma<W>(-s, s, q);
+    const fv_t<W> t = pk_fma<W>(e, h, s);
+#pragma unroll
+    for (int i = 0; i < W; ++i) dist[i] = __builtin_fmaxf(t[i], 0.0f);
+    // F.normalize: den = max(dist, 1e-12), div2_fast
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        den[i] = __builtin_amdgcn_fmed3f(dist[i], 1e-12f, __builtin_inff());
+        r[i] = __builtin_amdgcn_rcpf(den[i]);
+    }
+    r = pk_fma<W>(pk_fma<W>(-den, r, fvs<W>(1.0f)), r, r);
+    const fv_t<W> qx = dx * r, qy = dy * r;
+    const fv_t<W> nx = pk_fma<W>(pk_fma<W>(-den, qx, dx), r, qx);
+    const fv_t<W> ny = pk_fma<W>(pk_fma<W>(-den, qy, dy), r, qy);
+    // bearing_of<true>
+    const fv_t<W> dot0 = fvs<W>(dirx) * nx + fvs<W>(diry) * ny;
+#pragma unroll
+    for (int i = 0; i < W; ++i) dot[i] = __builtin_amdgcn_fmed3f(dot0[i], -1.0f, 1.0f);
+    const fv_t<W> orth = nx - dot * fvs<W>(dirx);
+    const fv_t<W> ac = acosv_dev<W>(dot);
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        const float g = (orth[i] > 0.0f ? -1.0f : 1.0f) * ac[i];
+        ang[i] = dist[i] < cap ? 0.0f : g;
+    }
+}
+
+__device__ __forceinline__ void pair2_fast(float ox, float oy, float dirx, float diry, f2_t px,
+                                           f2_t py, float cap, f2_t &dist, f2_t &ang)
+{
+    pairv_fast<2>(ox, oy, dirx, diry, px, py, cap, dist, ang);
+}
+
+// Vector width of pairs_fast's groups (MARLNAV_PACKED_W: A/B builds)
+#ifndef MARLNAV_PACKED_W
+#define MARLNAV_PACKED_W 4
+#endif
+
+// N pairs of one row (ox, oy, heading dirx, diry): groups of W pairs per
+// pairv_fast (then one of 2), the scalar FAST pair math on an odd last one
+template <int N, int W = MARLNAV_PACKED_W, int K0 = 0>
+__device__ __forceinline__ void pairs_fast(float ox, float oy, float dirx, float diry,
+                                           const float (&px)[N], const float (&py)[N], float cap,
+                                           float (&d)[N], float (&g)[N])
+{
+    constexpr int R = N - K0;
+    if constexpr (R >= 2) {
+        constexpr int V = R >= W ? W : (R >= 4 ? 4 : 2);
+        fv_t<V> vx, vy, vd, vg;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            vx[i] = px[K0 + i];
+            vy[i] = py[K0 + i];
+        }
+        pairv_fast<V>(ox, oy, dirx, diry, vx, vy, cap, vd, vg);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            d[K0 + i] = vd[i];
+            g[K0 + i] = vg[i];
+        }
+        pairs_fast<N, W, K0 + V>(ox, oy, dirx, diry, px, py, cap, d, g);
+    } else if constexpr (R == 1) {
+        bool unused = true;
+        d[N - 1] = pair_dist<true>(ox, oy, px[N - 1], py[N - 1], unused);
+        g[N - 1] = pair_angle<true>(ox, oy, px[N - 1], py[N - 1], dirx, diry, d[N - 1], cap, unused);
+    }
+}
+
 // Correctly rounded fp32 sin/cos of an angle already clamped to [-pi, pi]
 // (the heading update, environment.py:131-137). The reference evaluates
 // torch.sin/cos on its CPU path, which in this torch build is MKL VML
@@ -489,13 +631,40 @@ __device__ __forceinline__ void philox2x32_10(uint32_t &c0, uint32_t &c1, uint32
     }
 }
 
-// the 32-bit Philox key of block `blk` at step s: the 64-bit seed, the
-// block index and the high word of s (zero below 2^32 steps) folded by odd
-// multipliers (the counter carries the env id and the low word of s)
-__host__ __device__ constexpr uint32_t native_key(uint64_t seed, uint32_t blk, uint64_t s)
+// The caller's 64-bit seed enters the stream only through its splitmix64
+// finalisation (Steele, Lea, Flood, OOPSLA'14: a bijection of the 64-bit
+// words), done once per launch on the host (marlnav_step, marlnav_reinit_all
+// store it in the kernel's MarlnavParams.seed): seeds that differ in either
+// word give unrelated mixed seeds.
+__host__ __device__ constexpr uint64_t native_seed_mix(uint64_t seed)
 {
-    return (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x9E3779B1u) ^
-           ((uint32_t)(s >> 32) * 0xC2B2AE3Du) ^ (blk * 0x27D4EB2Fu);
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// murmur3's 32-bit finaliser (a bijection)
+__host__ __device__ constexpr uint32_t fmix32(uint32_t h)
+{
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    return h ^ (h >> 16);
+}
+
+// the 32-bit Philox key of block `blk` at step s from the MIXED seed m
+// (native_seed_mix): its low word XOR fmix32 of the block index, the high
+// word of s (zero below 2^32 steps) and m's high word. No linear relation
+// ties (seed, blk) to (seed', blk'): a key shared by two of them is a
+// 2^-32 coincidence of the hashes, not a shift of the block index. The
+// counter carries the env id and the low word of s. Where blk is
+// wave-uniform (the env-block kernel's draws) the key is SALU work.
+__host__ __device__ constexpr uint32_t native_key(uint64_t m, uint32_t blk, uint64_t s)
+{
+    return (uint32_t)m ^
+           fmix32(blk * 0x9E3779B1u + (uint32_t)(s >> 32) * 0x85EBCA77u + (uint32_t)(m >> 32));
 }
 
 // block `blk` of env gid at step s: two 32-bit words
@@ -992,6 +1161,63 @@ __device__ __forceinline__ RowOut observe_row_own(const float *__restrict__ sts,
                                                   float *row, const MarlnavParams &pr, bool &ok)
 {
     const float cap = pr.cap_distance;
+    if constexpr (FAST && MARLNAV_PACKED_PAIRS && !(MARLNAV_AB & 64)) {
+        // the row's pairs in row order - target, obstacles, other agents -
+        // two per pair2_fast (the same bits as pair_dist/pair_angle<true>,
+        // scripts/probes/pair_forms.hip); an odd last pair alone
+        constexpr int NP = 1 + O + (A - 1);
+        float px[NP], py[NP], pd[NP], pg[NP];
+        px[0] = tge[0];
+        py[0] = tge[1];
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+            px[1 + j] = obe[2 * j];
+            py[1 + j] = obe[2 * j + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < A - 1; ++j) {
+            const int m = j + (j >= a ? 1 : 0);
+            px[1 + O + j] = sts[5 * m];
+            py[1 + O + j] = sts[5 * m + 1];
+        }
+        pairs_fast<NP>(ox, oy, dx, dy, px, py, cap, pd, pg);
+        row[0] = pg[0];
+        row[1] = pd[0];
+        bool ob_risk = false, ob_col = false, ag_risk = false, ag_col = false;
+        float band = 0.0f;
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+            row[2 + j] = pg[1 + j];
+            row[2 + O + j] = pd[1 + j];
+            if (TERMS) {
+                ob_risk |= pd[1 + j] < pr.ob_risk_dist;
+                ob_col |= pd[1 + j] < pr.ob_coll_dist;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < A - 1; ++j) {
+            const float d = pd[1 + O + j];
+            row[2 + 2 * O + j] = pg[1 + O + j];
+            row[2 + 2 * O + (A - 1) + j] = d;
+            if (TERMS) {
+                ag_risk |= d < pr.ag_risk_dist;
+                ag_col |= d < pr.ag_coll_dist;
+                band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1.0f : 0.0f;
+            }
+        }
+        RowOut out{0.0f, 0.0f, 0u};
+        if (TERMS) {
+            const float *agd = row + 2 + 2 * O + (A - 1);
+            float bond;
+            if (pr.flags & kTermsFastFlag)
+                bond = torch_row_sum_r<A - 1>(agd, [&](float d) { return bond_term<true, REFC>(d, pr, ok); });
+            else
+                bond = torch_row_sum_r<A - 1>(agd, [&](float d) { return bond_term<false>(d, pr, ok); });
+            out = row_reward<A, FAST, REFC>(pg[0], pd[0], ob_risk || ag_risk, ob_col || ag_col, band,
+                                            bond, pr, ok);
+        }
+        return out;
+    }
     const float td = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
     const float ta = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, td, cap, ok);
     row[0] = ta;

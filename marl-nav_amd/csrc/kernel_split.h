@@ -286,6 +286,91 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     // SHARP1: bond_sharpness == 1 (the reference's constant, environment.py:
     // 66), where (d - ideal) / 1 is d - ideal exactly
     if constexpr (TERMS && TFAST && !SHARP1) d_sharp = make_divc(pr.bond_sharpness, ok);
+    if constexpr (FAST && MARLNAV_PACKED_PAIRS && !(MARLNAV_AB & 64)) {
+        // every slot's pair first - two per pair2_fast (pairs_fast); a slot
+        // with no pair (j >= O, or kx >= A - 1 off the target lane) computes
+        // a discarded one - then the row writes and terms of the loops below
+        constexpr bool TS = !kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>;
+        constexpr int T0 = TS ? 1 : 0, N = T0 + SP::NOB + SP::NAG;
+        float px[N], py[N], pd[N], pg[N];
+        if constexpr (TS) {
+            px[0] = tge[0];
+            py[0] = tge[1];
+        }
+#pragma unroll
+        for (int i = 0; i < SP::NOB; ++i) {
+            const int j = q + LPR * i;
+            const bool valid = O % LPR == 0 || j < O;
+            const bool tgt = kSplitTgtInOb<A, O, LPR> && i == SP::NOB - 1 && q == TQ;
+            const float *pt = tgt ? tge : obe + 2 * (valid ? j : 0);
+            px[T0 + i] = pt[0];
+            py[T0 + i] = pt[1];
+        }
+#pragma unroll
+        for (int i = 0; i < SP::NAG; ++i) {
+            const int kx = q + LPR * i;
+            const bool valid = (A - 1) % LPR == 0 || kx < A - 1;
+            const bool tgt = kSplitTgtInAg<A, O, LPR> && i == SP::NAG - 1 && q == TQ;
+            const int m = valid ? kx + (kx >= a ? 1 : 0) : 0;
+            const float *pt = tgt ? tge : sts + 5 * m;
+            px[T0 + SP::NOB + i] = pt[0];
+            py[T0 + SP::NOB + i] = pt[1];
+        }
+        pairs_fast<N>(ox, oy, dx, dy, px, py, cap, pd, pg);
+        if constexpr (TS) {
+            t.ta = pg[0];
+            t.td = pd[0];
+            if (q == 0) {
+                orow[0] = pg[0];
+                orow[1] = pd[0];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < SP::NOB; ++i) {
+            const int j = q + LPR * i;
+            const bool valid = O % LPR == 0 || j < O;
+            const bool tgt = kSplitTgtInOb<A, O, LPR> && i == SP::NOB - 1 && q == TQ;
+            const float d = pd[T0 + i], ang = pg[T0 + i];
+            if (valid) {
+                orow[2 + j] = ang;
+                orow[2 + O + j] = d;
+                if (TERMS) ob_min = __builtin_fminf(ob_min, d);
+            } else if (tgt) {
+                orow[0] = ang;
+                orow[1] = d;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < SP::NAG; ++i) {
+            const int kx = q + LPR * i;
+            const bool valid = (A - 1) % LPR == 0 || kx < A - 1;
+            const bool tgt = kSplitTgtInAg<A, O, LPR> && i == SP::NAG - 1 && q == TQ;
+            const float d = pd[T0 + SP::NOB + i], ang = pg[T0 + SP::NOB + i];
+            if (valid) {
+                orow[2 + 2 * O + kx] = ang;
+                orow[2 + 2 * O + (A - 1) + kx] = d;
+                if (TERMS) {
+                    ag_min = __builtin_fminf(ag_min, d);
+                    t.band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1 : 0;
+                    if constexpr (TFAST) {
+                        const float sd = SHARP1 ? d - pr.ideal_dist
+                                                : div_c(d - pr.ideal_dist, d_sharp, ok);
+                        bond_row[kx] = recip_fast(1.0f + sd * sd, ok);
+                    } else {
+                        const float sd = (d - pr.ideal_dist) / pr.bond_sharpness;
+                        bond_row[kx] = 1.0f / (1.0f + sd * sd);
+                    }
+                }
+            } else if (tgt) {
+                orow[0] = ang;
+                orow[1] = d;
+            }
+        }
+        if (TERMS)
+            t.fl |= (ob_min < pr.ob_risk_dist ? 1u : 0u) | (ob_min < pr.ob_coll_dist ? 2u : 0u) |
+                    (ag_min < pr.ag_risk_dist ? 4u : 0u) | (ag_min < pr.ag_coll_dist ? 8u : 0u);
+        return t;
+    }
     if constexpr (!kSplitTgtInAg<A, O, LPR> && !kSplitTgtInOb<A, O, LPR>) {
         const float d = pair_dist<FAST>(ox, oy, tge[0], tge[1], ok);
         const float ang = pair_angle<FAST>(ox, oy, tge[0], tge[1], dx, dy, d, cap, ok);

@@ -141,3 +141,9 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_EARLY_OUT
 #define MARLNAV_EARLY_OUT -1
 #endif
+// Packed pair math (pair2_fast: two pairs of a row per v_pk_*_f32) in the
+// coordinate-checked observation of the env-block kernel (1), or one pair per
+// VALU instruction (0; A/B builds). scripts/probes/pair_forms.hip.
+#ifndef MARLNAV_PACKED_PAIRS
+#define MARLNAV_PACKED_PAIRS 1
+#endif

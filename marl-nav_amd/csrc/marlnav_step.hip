@@ -566,6 +566,7 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
 {
     if (!pr_in) return fail(MARLNAV_EINVAL, "params/buffers is NULL");
     MarlnavParams prm = *pr_in;
+    prm.seed = native_seed_mix(prm.seed);  // the kernels key the native stream by the mixed seed
     prm.flags &= ~(kTermsFastFlag | kWriteThroughFlag);
     if (terms_fast_params(prm)) prm.flags |= kTermsFastFlag;
     const MarlnavParams *pr = &prm;
@@ -669,9 +670,11 @@ int marlnav_reinit_all(const MarlnavDims *d, const MarlnavParams *pr, const floa
     if (!pr || !formation || !states || !obstacles || !target)
         return fail(MARLNAV_EINVAL, "a required reinit buffer is NULL");
     const unsigned blocks = (unsigned)((d->num_parallel + 255) / 256);
+    MarlnavParams prm = *pr;
+    prm.seed = native_seed_mix(prm.seed);  // as marlnav_step
     hipLaunchKernelGGL(reinit_all_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        d->num_parallel, d->num_agents, d->obstacle_stride, d->env_offset,
-                       step_idx, *pr, formation, states, obstacles, target);
+                       step_idx, prm, formation, states, obstacles, target);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(MARLNAV_ELAUNCH, "marlnav_reinit_all: %s", hipGetErrorString(e));

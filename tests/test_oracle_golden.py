@@ -259,6 +259,51 @@ def test_native_stream_definition():
     assert len(keys) == 64
 
 
+def _splitmix64(x):
+    m = (1 << 64) - 1
+    z = (x + 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def _fmix32(h):
+    m = (1 << 32) - 1
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & m
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & m
+    return h ^ (h >> 16)
+
+
+def test_native_key_seed_mixing():
+    """The native key uses the whole 64-bit seed through a nonlinear mix
+    (ADVICE r5): native_key(seed, blk, s) = lo32(m) ^ fmix32(blk * 0x9E3779B1
+    + hi32(s) * 0x85EBCA77 + hi32(m)), m = splitmix64(seed) - restated here in
+    Python against the oracle. Seeds differing only in the high word, the
+    round-5 colliding pair (1 << 32, 0x9E3779B1), and shifted block indices
+    (key(seed, j) == key(seed ^ j * 0x27D4EB2F, 0) held for the linear key)
+    all give distinct keys."""
+    m32 = (1 << 32) - 1
+    for seed in (0, 1, 1 << 32, 0x9E3779B1, 0x123456789ABCDEF, m32, (1 << 64) - 1):
+        for blk, s in ((0, 0), (5, 0), (3, (7 << 32) + 1)):
+            m = _splitmix64(seed)
+            want = (m & m32) ^ _fmix32((blk * 0x9E3779B1 + (s >> 32) * 0x85EBCA77 + (m >> 32)) & m32)
+            assert orc.native_key(seed, blk, s) == want, (seed, blk, s)
+    assert orc.native_key(1 << 32, 0, 0) != orc.native_key(0x9E3779B1, 0, 0)
+    # hi-word-only differences: 4096 seeds, one key each, all distinct
+    hi_keys = {orc.native_key(h << 32, 0, 0) for h in range(4096)}
+    lo_keys = {orc.native_key(h, 0, 0) for h in range(4096)}
+    assert len(hi_keys) == 4096 and len(lo_keys) == 4096
+    # the linear key's block shift no longer aliases obstacle j onto obstacle 0
+    seed = 0x0123456789ABCDEF
+    for j in range(1, 64):
+        assert orc.native_key(seed, j, 0) != orc.native_key(seed ^ ((j * 0x27D4EB2F) & m32), 0, 0)
+    # blocks x seeds: 64 x 256 keys without a collision
+    grid = {orc.native_key(sd * 0x10001, j, 0) for sd in range(256) for j in range(64)}
+    assert len(grid) == 64 * 256
+
+
 def test_oracle_sincos_correctly_rounded():
     """oracle_sincos (= the kernel's sincos_k, same operations) is the
     correctly rounded fp32 sin/cos: against long double sinl/cosl rounded to
