@@ -394,141 +394,102 @@ __device__ __forceinline__ float pair_angle(float ox, float oy, float px, float 
 }
 
 // ------------------------------------------------- packed pair math (FAST)
-// W pairs of one row per vector: the operations of pair_dist<true> +
+// Two pairs of one row per instruction: the operations of pair_dist<true> +
 // pair_angle<true> (and of the device acosf, op for op as acos_device in the
-// oracle restates it) on W-wide clang vectors, which the backend lowers to
-// W/2 independent v_pk_add/mul/fma_f32 per step - two fp32 operations per
-// lane-slot where a VOP2 f32 instruction takes one, and (W >= 4) no packed
-// instruction waiting on the one before it (a dependent packed pair costs an
-// s_nop on gfx950). The per-element steps that have no packed form (v_rsq,
-// v_rcp, v_sqrt, v_max/v_med3, compares, selects) stay per element. Every
-// packed operation is the same IEEE single operation per element as its
-// scalar twin (no contraction: -ffp-contract=off, explicit fma), so the
-// results are the scalar path's bits (scripts/probes/pair_forms.hip checks
-// 2^28 random pairs, the GPU suite every kernel output against the oracle).
-// No range guard: callers are coordinate-checked (FAST) blocks and tiles.
-template <int W>
-using fv_t = float __attribute__((ext_vector_type(W)));
-typedef fv_t<2> f2_t;
+// oracle restates it) on (pair a, pair b) lanes of v_pk_add/mul/fma_f32,
+// which take two fp32 operations per lane-slot where a VOP2 f32 instruction
+// takes one. The per-element steps that have no packed form on gfx950
+// (v_rsq/v_rcp/v_sqrt, v_max/v_med3, compares and selects) stay per element.
+// Every packed operation is the same IEEE single operation per element as
+// its scalar twin (no contraction: -ffp-contract=off, explicit fma), so the
+// results are the scalar path's bits (scripts/probes/pair_forms.hip: 2^28
+// random pair sets; the GPU suite: every kernel output against the oracle).
+// No range guard: callers are coordinate-checked (FAST) blocks.
+// Written with explicit .x/.y elements: the same math over generic W-wide
+// clang vectors (W = 2, 4, 6) compiled to dependent packed instructions
+// back to back, each pair of them separated by an s_nop, and measured
+// slower (profiles/r06_pair_forms_widths.txt, r06_ab_packed_widths.txt).
+typedef float f2_t __attribute__((ext_vector_type(2)));
 
-template <int W>
-__device__ __forceinline__ fv_t<W> pk_fma(fv_t<W> a, fv_t<W> b, fv_t<W> c)
+__device__ __forceinline__ f2_t pk_fma(f2_t a, f2_t b, f2_t c)
 {
     return __builtin_elementwise_fma(a, b, c);
 }
 
-template <int W>
-__device__ __forceinline__ fv_t<W> fvs(float x)
-{
-    return (fv_t<W>)(x);
-}
+__device__ __forceinline__ f2_t f2s(float x) { return f2_t{x, x}; }
 
 // the device library's acosf (ocml), op for op (acos_device in the oracle):
 // r = |x| > 0.5 ? 0.5 - 0.5|x| : x*x; u = r P5(r); |x| <= 0.5: pi/2 - (x +
 // x u); else 2(s + s u), or pi minus that for x < 0, s = v_sqrt_f32(r)
-template <int W>
-__device__ __forceinline__ fv_t<W> acosv_dev(fv_t<W> x)
+__device__ __forceinline__ f2_t acos2_dev(f2_t x)
 {
-    fv_t<W> ax, r, sq, out;
-#pragma unroll
-    for (int i = 0; i < W; ++i) ax[i] = __builtin_fabsf(x[i]);
-    const fv_t<W> rt = pk_fma<W>(ax, fvs<W>(-0.5f), fvs<W>(0.5f));
-    const fv_t<W> x2 = x * x;
-#pragma unroll
-    for (int i = 0; i < W; ++i) r[i] = ax[i] > 0.5f ? rt[i] : x2[i];
-    fv_t<W> p = pk_fma<W>(fvs<W>(__uint_as_float(0x3d1c21a7u)), r, fvs<W>(__uint_as_float(0x3c5fc5dau)));
-    p = pk_fma<W>(r, p, fvs<W>(__uint_as_float(0x3d034c3cu)));
-    p = pk_fma<W>(r, p, fvs<W>(__uint_as_float(0x3d3641b1u)));
-    p = pk_fma<W>(r, p, fvs<W>(__uint_as_float(0x3d999bc8u)));
-    p = pk_fma<W>(r, p, fvs<W>(__uint_as_float(0x3e2aaaacu)));
-    const fv_t<W> u = r * p;
-#pragma unroll
-    for (int i = 0; i < W; ++i) sq[i] = __builtin_amdgcn_sqrtf(r[i]);
-    const fv_t<W> s2 = pk_fma<W>(sq, u, sq);
-    const fv_t<W> zt = s2 + s2;
-    const fv_t<W> ztn = fvs<W>(__uint_as_float(0x40490fdbu)) - zt;
-    const fv_t<W> zs = fvs<W>(__uint_as_float(0x3fc90fdbu)) - pk_fma<W>(x, u, x);
-#pragma unroll
-    for (int i = 0; i < W; ++i) out[i] = ax[i] > 0.5f ? (x[i] < 0.0f ? ztn[i] : zt[i]) : zs[i];
-    return out;
+    const f2_t ax = f2_t{__builtin_fabsf(x.x), __builtin_fabsf(x.y)};
+    const f2_t rt = pk_fma(ax, f2s(-0.5f), f2s(0.5f));
+    const f2_t x2 = x * x;
+    const bool big0 = ax.x > 0.5f, big1 = ax.y > 0.5f;
+    const f2_t r = f2_t{big0 ? rt.x : x2.x, big1 ? rt.y : x2.y};
+    f2_t p = pk_fma(f2s(__uint_as_float(0x3d1c21a7u)), r, f2s(__uint_as_float(0x3c5fc5dau)));
+    p = pk_fma(r, p, f2s(__uint_as_float(0x3d034c3cu)));
+    p = pk_fma(r, p, f2s(__uint_as_float(0x3d3641b1u)));
+    p = pk_fma(r, p, f2s(__uint_as_float(0x3d999bc8u)));
+    p = pk_fma(r, p, f2s(__uint_as_float(0x3e2aaaacu)));
+    const f2_t u = r * p;
+    const f2_t sq = f2_t{__builtin_amdgcn_sqrtf(r.x), __builtin_amdgcn_sqrtf(r.y)};
+    const f2_t s2 = pk_fma(sq, u, sq);
+    const f2_t zt = s2 + s2;
+    const f2_t ztn = f2s(__uint_as_float(0x40490fdbu)) - zt;
+    const f2_t zs = f2s(__uint_as_float(0x3fc90fdbu)) - pk_fma(x, u, x);
+    return f2_t{big0 ? (x.x < 0.0f ? ztn.x : zt.x) : zs.x, big1 ? (x.y < 0.0f ? ztn.y : zt.y) : zs.y};
 }
 
-// pair_dist<true> and pair_angle<true> of W pairs (px, py) of the row at
+// pair_dist<true> and pair_angle<true> of two pairs (px, py) of the row at
 // (ox, oy) heading (dirx, diry): the distances and the capped bearings
-template <int W>
-__device__ __forceinline__ void pairv_fast(float ox, float oy, float dirx, float diry,
-                                           fv_t<W> px, fv_t<W> py, float cap, fv_t<W> &dist,
-                                           fv_t<W> &ang)
-{
-    const fv_t<W> dx = px - fvs<W>(ox), dy = py - fvs<W>(oy);
-    const fv_t<W> q = pk_fma<W>(dy, dy, dx * dx);
-    // sqrt_fast: rsq, one FMA-residual correction, max(., 0)
-    fv_t<W> y, den, r, dot;
-#pragma unroll
-    for (int i = 0; i < W; ++i) y[i] = __builtin_amdgcn_rsqf(q[i]);
-    const fv_t<W> s = q * y, h = fvs<W>(0.5f) * y;
-    const fv_t<W> e = pk_fma<W>(-s, s, q);
-    const fv_t<W> t = pk_fma<W>(e, h, s);
-#pragma unroll
-    for (int i = 0; i < W; ++i) dist[i] = __builtin_fmaxf(t[i], 0.0f);
-    // F.normalize: den = max(dist, 1e-12), div2_fast
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        den[i] = __builtin_amdgcn_fmed3f(dist[i], 1e-12f, __builtin_inff());
-        r[i] = __builtin_amdgcn_rcpf(den[i]);
-    }
-    r = pk_fma<W>(pk_fma<W>(-den, r, fvs<W>(1.0f)), r, r);
-    const fv_t<W> qx = dx * r, qy = dy * r;
-    const fv_t<W> nx = pk_fma<W>(pk_fma<W>(-den, qx, dx), r, qx);
-    const fv_t<W> ny = pk_fma<W>(pk_fma<W>(-den, qy, dy), r, qy);
-    // bearing_of<true>
-    const fv_t<W> dot0 = fvs<W>(dirx) * nx + fvs<W>(diry) * ny;
-#pragma unroll
-    for (int i = 0; i < W; ++i) dot[i] = __builtin_amdgcn_fmed3f(dot0[i], -1.0f, 1.0f);
-    const fv_t<W> orth = nx - dot * fvs<W>(dirx);
-    const fv_t<W> ac = acosv_dev<W>(dot);
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        const float g = (orth[i] > 0.0f ? -1.0f : 1.0f) * ac[i];
-        ang[i] = dist[i] < cap ? 0.0f : g;
-    }
-}
-
 __device__ __forceinline__ void pair2_fast(float ox, float oy, float dirx, float diry, f2_t px,
                                            f2_t py, float cap, f2_t &dist, f2_t &ang)
 {
-    pairv_fast<2>(ox, oy, dirx, diry, px, py, cap, dist, ang);
+    const f2_t dx = px - f2s(ox), dy = py - f2s(oy);
+    const f2_t q = pk_fma(dy, dy, dx * dx);
+    // sqrt_fast: rsq, one FMA-residual correction, max(., 0)
+    const f2_t y = f2_t{__builtin_amdgcn_rsqf(q.x), __builtin_amdgcn_rsqf(q.y)};
+    const f2_t s = q * y, h = f2s(0.5f) * y;
+    const f2_t e = pk_fma(-s, s, q);
+    const f2_t t = pk_fma(e, h, s);
+    dist = f2_t{__builtin_fmaxf(t.x, 0.0f), __builtin_fmaxf(t.y, 0.0f)};
+    // F.normalize: den = max(dist, 1e-12), div2_fast
+    const f2_t den = f2_t{__builtin_amdgcn_fmed3f(dist.x, 1e-12f, __builtin_inff()),
+                          __builtin_amdgcn_fmed3f(dist.y, 1e-12f, __builtin_inff())};
+    f2_t r = f2_t{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    r = pk_fma(pk_fma(-den, r, f2s(1.0f)), r, r);
+    const f2_t qx = dx * r, qy = dy * r;
+    const f2_t nx = pk_fma(pk_fma(-den, qx, dx), r, qx);
+    const f2_t ny = pk_fma(pk_fma(-den, qy, dy), r, qy);
+    // bearing_of<true>
+    f2_t dot = f2s(dirx) * nx + f2s(diry) * ny;
+    dot = f2_t{__builtin_amdgcn_fmed3f(dot.x, -1.0f, 1.0f), __builtin_amdgcn_fmed3f(dot.y, -1.0f, 1.0f)};
+    const f2_t orth = nx - dot * f2s(dirx);
+    const f2_t ac = acos2_dev(dot);
+    const float a0 = (orth.x > 0.0f ? -1.0f : 1.0f) * ac.x;
+    const float a1 = (orth.y > 0.0f ? -1.0f : 1.0f) * ac.y;
+    ang = f2_t{dist.x < cap ? 0.0f : a0, dist.y < cap ? 0.0f : a1};
 }
 
-// Vector width of pairs_fast's groups (MARLNAV_PACKED_W: A/B builds)
-#ifndef MARLNAV_PACKED_W
-#define MARLNAV_PACKED_W 4
-#endif
-
-// N pairs of one row (ox, oy, heading dirx, diry): groups of W pairs per
-// pairv_fast (then one of 2), the scalar FAST pair math on an odd last one
-template <int N, int W = MARLNAV_PACKED_W, int K0 = 0>
+// N pairs of one row (ox, oy, heading dirx, diry): pair2_fast on pairs
+// (0, 1), (2, 3), ... and the scalar FAST pair math on an odd last one
+template <int N>
 __device__ __forceinline__ void pairs_fast(float ox, float oy, float dirx, float diry,
                                            const float (&px)[N], const float (&py)[N], float cap,
                                            float (&d)[N], float (&g)[N])
 {
-    constexpr int R = N - K0;
-    if constexpr (R >= 2) {
-        constexpr int V = R >= W ? W : (R >= 4 ? 4 : 2);
-        fv_t<V> vx, vy, vd, vg;
 #pragma unroll
-        for (int i = 0; i < V; ++i) {
-            vx[i] = px[K0 + i];
-            vy[i] = py[K0 + i];
-        }
-        pairv_fast<V>(ox, oy, dirx, diry, vx, vy, cap, vd, vg);
-#pragma unroll
-        for (int i = 0; i < V; ++i) {
-            d[K0 + i] = vd[i];
-            g[K0 + i] = vg[i];
-        }
-        pairs_fast<N, W, K0 + V>(ox, oy, dirx, diry, px, py, cap, d, g);
-    } else if constexpr (R == 1) {
+    for (int k = 0; k + 1 < N; k += 2) {
+        f2_t d2, g2;
+        pair2_fast(ox, oy, dirx, diry, f2_t{px[k], px[k + 1]}, f2_t{py[k], py[k + 1]}, cap, d2, g2);
+        d[k] = d2.x;
+        d[k + 1] = d2.y;
+        g[k] = g2.x;
+        g[k + 1] = g2.y;
+    }
+    if constexpr (N % 2 != 0) {
         bool unused = true;
         d[N - 1] = pair_dist<true>(ox, oy, px[N - 1], py[N - 1], unused);
         g[N - 1] = pair_angle<true>(ox, oy, px[N - 1], py[N - 1], dirx, diry, d[N - 1], cap, unused);

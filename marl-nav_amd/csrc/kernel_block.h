@@ -341,12 +341,17 @@ __global__ void __launch_bounds__(64 * (A + HELP))
         }
         float a0 = actw[lane];
         a1 = actw[E + lane];
+        STAMPS_S(0);  // (substamps: this wave's actions landed)
         if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
             KArgsK *kl = kargs_late<kHotKargsOff>();
             a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
             a1 = kl->p.act_scale[1] * a1 + kl->p.act_mean[1];
         }
         sincos_k(clamp_t(a0, -kPiF, kPiF), &sn, &c);
+#if MARLNAV_STAMPS && MARLNAV_SUBSTAMPS
+        asm volatile("" ::"v"(sn), "v"(c));
+#endif
+        STAMPS_S(1);  // (substamps: the heading's sin/cos done)
     }
     const int l = (int)lane;  // env of this lane within the block
     const int r = l * A + (hw ? 0 : w);  // row of this lane (the draw wave has none)
@@ -355,6 +360,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
     if (tid == 0) *bad_word = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+    STAMPS_S(2);  // (substamps: every span this wave issued landed)
     __syncthreads();
     STAMP(1);
     if (MARLNAV_AB & 8192) {  // (AB 8192: timing / census only - staged, then exit;
@@ -440,6 +446,10 @@ __global__ void __launch_bounds__(64 * (A + HELP))
             ro = observe_row_own<A, O, !OBS_ONLY, false>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
                                                          lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
                                                          rowv, pr, unused);
+#if MARLNAV_STAMPS && MARLNAV_SUBSTAMPS
+        asm volatile("" ::"v"(ro.r_miss), "v"(rowv[0]), "v"(rowv[D - 1]));
+#endif
+        STAMPS_S(3);  // (substamps: this lane's row computed)
         lds_row_write<D>(obs_rows + r * D, rowv);
         if (!OBS_ONLY) red[r] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
     }
@@ -620,8 +630,13 @@ __global__ void __launch_bounds__(64 * (A + HELP))
         }
     }
     STAMP(5);
+    // the one barrier after the per-env phase: the fused normaliser of a
+    // block whose rows do not divide over its threads (partial block, or NT
+    // not a multiple of D) stages mean and scale in LDS; every wave of the
+    // block, the draw wave included, decides from this one value
+    const bool norm_barrier = !OBS_ONLY && norm && !(full && NT % D == 0);
     if (hw) {  // (the draw wave stores nothing; it meets the norm path's barrier)
-        if (!OBS_ONLY && !(full && !norm) && !(full && NT % D == 0) && norm) __syncthreads();
+        if (norm_barrier) __syncthreads();
     } else if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
         if (!(MARLNAV_AB & 2) && !early)
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)),
@@ -631,7 +646,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
         // thread tid only ever meets feature tid % D (NT is a multiple of D),
         // so its mean and scale are loaded once; every LDS read and every
         // division is issued ahead of the stores
-        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(b.states_out + e0 * (A * 5)),
+        block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)),
                                                st, tid, wt);
         KArgsK *kl = kargs_late<kHotKargsOff>();
         const int kk = tid % D;
@@ -653,7 +668,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
         }
     } else if (!OBS_ONLY) {
         block_store(gobs, obs_rows, nrow * D, tid, NT, wt);
-        if (norm) {
+        if (norm_barrier) {  // (here: norm)
             // mean and scale staged in LDS once (the reward-term slots are
             // free after the per-env phase), then one pass over the rows
             KArgsK *kl = kargs_late<kHotKargsOff>();
@@ -676,7 +691,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
                     gn[i] = v;
             }
         }
-        block_store(in_sgpr(b.states_out + e0 * (A * 5)), st, nrow * 5, tid, NT, wt);
+        block_store(in_sgpr(bo.states_out + e0 * (A * 5)), st, nrow * 5, tid, NT, wt);
     }
     STAMP(6);
 #if MARLNAV_STAMPS

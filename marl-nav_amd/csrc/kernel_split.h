@@ -286,7 +286,7 @@ __device__ __forceinline__ SplitTerms split_pairs(const float *__restrict__ sts,
     // SHARP1: bond_sharpness == 1 (the reference's constant, environment.py:
     // 66), where (d - ideal) / 1 is d - ideal exactly
     if constexpr (TERMS && TFAST && !SHARP1) d_sharp = make_divc(pr.bond_sharpness, ok);
-    if constexpr (FAST && MARLNAV_PACKED_PAIRS && !(MARLNAV_AB & 64)) {
+    if constexpr (FAST && MARLNAV_PACKED_SPLIT && !(MARLNAV_AB & 64)) {
         // every slot's pair first - two per pair2_fast (pairs_fast); a slot
         // with no pair (j >= O, or kx >= A - 1 off the target lane) computes
         // a discarded one - then the row writes and terms of the loops below
@@ -652,6 +652,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
 {
     using SP = SplitPlan<A, O, LPR>;
     constexpr int EPW = SP::EPW, R = SP::R, D = SP::D;
+    // the own-wave path stores raw row terms for wave 0's row_reward, which
+    // wave 0 applies only when the row leaders do not (kSplitRRLeader)
+    static_assert(!kSplitOwn<A, O, LPR, OWN> || !kSplitRRLeader<A, O>,
+                  "kSplitOwn needs wave 0's row rewards (MARLNAV_SPLIT_RR_LEADER=0)");
     (void)k;  // read through kargs_late<kHotKargsOff>()
     extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS

@@ -23,12 +23,31 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
             sp_[2 * (k) + 1] = clock64();                                          \
         }                                                                          \
     } while (0)
-// extra realtime-only stamps at slots 20..23 (diagnostic sub-phases)
-#define STAMPX(k)                                                                  \
+// extra realtime-only stamps at slots 20..23 (diagnostic sub-phases): the
+// per-env / re-init sub-phases (STAMPX), or with MARLNAV_SUBSTAMPS=1 the
+// env-block kernel's stage and observe sub-phases (STAMPS_S) instead
+#ifndef MARLNAV_SUBSTAMPS
+#define MARLNAV_SUBSTAMPS 0
+#endif
+#define STAMP_SLOT_(k)                                                             \
     do {                                                                           \
         if (lane == 0) *STAMP_PTR((size_t)gw * 24 + 20 + (k)) = wall_clock64();    \
     } while (0)
+#if MARLNAV_SUBSTAMPS
+#define STAMPX(k) \
+    do {          \
+    } while (0)
+#define STAMPS_S(k) STAMP_SLOT_(k)
 #else
+#define STAMPX(k) STAMP_SLOT_(k)
+#define STAMPS_S(k) \
+    do {            \
+    } while (0)
+#endif
+#else
+#define STAMPS_S(k) \
+    do {            \
+    } while (0)
 #define STAMPX(k) \
     do {          \
     } while (0)
@@ -143,7 +162,15 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #endif
 // Packed pair math (pair2_fast: two pairs of a row per v_pk_*_f32) in the
 // coordinate-checked observation of the env-block kernel (1), or one pair per
-// VALU instruction (0; A/B builds). scripts/probes/pair_forms.hip.
+// VALU instruction (0; A/B builds). scripts/probes/pair_forms.hip. Same box,
+// graph replay, steady (profiles/r06_ab_packed.txt): 131072x3x8 16.61 ->
+// 16.06 us, 65536x3x3 6.36 -> 6.35, 16384x3x3 4.62 -> 4.61.
 #ifndef MARLNAV_PACKED_PAIRS
 #define MARLNAV_PACKED_PAIRS 1
+#endif
+// The same in the pair-split kernel's split_pairs (A16/O32, A3/O8 small
+// grids): 4096x16x32 11.19 -> 11.33 us, 1024x3x8 and 2048x16x32 unchanged
+// (profiles/r06_ab_packed_split.txt): off (A/B builds: 1)
+#ifndef MARLNAV_PACKED_SPLIT
+#define MARLNAV_PACKED_SPLIT 0
 #endif

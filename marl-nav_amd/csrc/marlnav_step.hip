@@ -365,13 +365,30 @@ int launch_split(const SplitVariant &v, BlockFn fn, const StepArgs &args, const 
 }
 
 // env-block kernels (block_kernel) for these shapes
-constexpr int64_t kDrawWaveMaxBlocks = 256;
 struct BlockVariant {
     int A, O;
     BlockFn step, obs, noisy;
     size_t lds;
     BlockFn step_draw;  // (or null) the step with a draw wave: grids of at most one block per CU
+    int E;              // envs per block
 };
+
+// compute units of the current device (the draw-wave rule: at most one
+// block per CU), read once per device
+int device_cus()
+{
+    static std::atomic<int> cached[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    int n = cached[dev].load(std::memory_order_relaxed);
+    if (n <= 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;  // MI355X
+        cached[dev].store(n, std::memory_order_relaxed);
+    }
+    return n;
+}
 
 // The draw-wave instantiation (block_kernel HELP): the native re-init's
 // fresh-obstacle draws move from the agent waves' stage to a fourth wave on
@@ -386,7 +403,7 @@ constexpr BlockFn block_draw_fn()
 #define MARLNAV_BLOCK_VARIANT(A, O)                                                    \
     {A, O, block_kernel<A, O, false, false>, block_kernel<A, O, true, false>,          \
      block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4,             \
-     block_draw_fn<A, O>()}
+     block_draw_fn<A, O>(), BlockPlan<A, O>::E}
 const BlockVariant kBlockVariants[] = {
     MARLNAV_BLOCK_VARIANT(3, 3),
     MARLNAV_BLOCK_VARIANT(3, 8),
@@ -417,7 +434,7 @@ int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const 
     KArgs ka;
     ka.a = args;
     ka.p = pr;
-    ka.a.W = BlockPlan<3, 3>::E;
+    ka.a.W = v.E;
     ka.a.ntiles = (args.P + ka.a.W - 1) / ka.a.W;
     // the leading arguments (kHotKargsOff, kernel_args.h): staging pointers, P
     float *h_states = args.b.states;
@@ -616,8 +633,8 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
         if (const BlockVariant *v = select_block(d, args.b, false)) {
             g_last_family = MARLNAV_FAMILY_BLOCK;
             // one block per CU (MI355X: 256 CUs) leaves a SIMD of each CU idle
-            const int64_t nblk = (d->num_parallel + BlockPlan<3, 3>::E - 1) / BlockPlan<3, 3>::E;
-            if (!noisy && v->step_draw && nblk <= kDrawWaveMaxBlocks && !b->fresh_states)
+            const int64_t nblk = (d->num_parallel + v->E - 1) / v->E;
+            if (!noisy && v->step_draw && nblk <= device_cus() && !b->fresh_states)
                 return launch_block(*v, v->step_draw, args, *pr, stream, "marlnav_step", v->A + 1);
             return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-4 evidence on one GPU box: GPU tests, smoke, the bench line at the
+# A round's evidence set on one GPU box (TAG names it, e.g. TAG=r06_end):
+# GPU tests, smoke, the bench line at the
 # driver's shape (twice) and at 500 steps with the CPU baseline, rocprofv3
 # kernel stats of the bench at configs[2] and at configs[4]'s per-GPU shape
 # and of configs[3], graph-replay step times of every BASELINE config, PMC of
@@ -11,7 +12,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out
-TAG=${TAG:-r04}
+TAG=${TAG:-evidence}
 mkdir -p "$OUT"
 fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 step() {  # name timeout cmd...
@@ -37,6 +38,8 @@ if on PROF; then
       -- python bench.py --steps 200 --warmup 20 --cpu-baseline off
   step rocprof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4_$TAG -o run \
       -- python bench.py --envs 16384 --steps 200 --warmup 20 --cpu-baseline off
+  step rocprof_2m 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_2m_$TAG -o run \
+      -- python scripts/pmc_run.py 2097152x3x3 300
   step rocprof_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3_$TAG -o run \
       -- python scripts/pmc_run.py 4096x16x32 200
 fi
@@ -51,4 +54,4 @@ if on DIST; then
   MARLNAV_BENCH_BACKEND=gloo step bench_gloo2 300 python bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 3
   step bench_gloo8_c4 400 python bench.py --gpus 8 --config 4 --steps 20 --warmup 5 --cpu-seconds 3
 fi
-echo round_end done
+echo evidence done

@@ -170,6 +170,24 @@ def main():
                       round(float(np.median(ph[reo][m, 3])), 3), "sub-phases", out,
                       "nfin histogram", {int(k): int(v) for k, v in
                                          zip(*np.unique(raw[reo][m, 19], return_counts=True))})
+        # SUB=1 (substamps.so): the stage and observe sub-phases of every
+        # agent wave (STAMPS_S slots 20..23: actions landed, sin/cos done,
+        # spans landed; row computed)
+        if os.environ.get("SUB") == "1":
+            x = raw[:, 20:24] * 10.0 / 1e3
+            ok = (x > 0).all(axis=1)
+            if ok.any():
+                seq = [("t0", rt[:, 0]), ("actions_landed", x[:, 0]), ("sincos_done", x[:, 1]),
+                       ("spans_landed", x[:, 2]), ("stage_barrier", rt[:, 1]),
+                       ("move_barrier", rt[:, 2]), ("row_computed", x[:, 3]),
+                       ("observe_barrier", rt[:, 3])]
+                for q in (50, 90):
+                    out = {f"{a}->{b}": round(float(np.percentile((tb - ta)[ok], q)), 3)
+                           for (a, ta), (b, tb) in zip(seq, seq[1:])}
+                    print(cfg, f"stage/observe sub-phases (p{q} us, {int(ok.sum())} waves):", out)
+                print(cfg, "entry->t0 median us", round(float(np.median((rt[:, 0] - entry)[ok])), 3))
+            del env
+            continue
         # wave 0's per-env phase (STAMPX 0..2 in wave 0: reward terms read,
         # outputs issued, list / counters done), every block
         w0 = (gidx % int(os.environ.get("WPB", str(A)))) == 0

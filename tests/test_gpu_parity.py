@@ -1335,12 +1335,16 @@ def test_c_host_matches_python_env(pkg, P, A, O, steps, tmp_path):
     assert counters[0] > 0  # the 5-step episodes truncated
 
 
-@pytest.mark.parametrize("P,A,O", [(4096, 3, 3), (2048 + 5, 3, 8), (60, 3, 3), (512, 16, 32)])
+@pytest.mark.parametrize("P,A,O", [(4096, 3, 3), (2048 + 5, 3, 8), (60, 3, 3), (512, 16, 32),
+                                   (16384, 3, 3), (16001, 3, 3)])
 def test_fused_normalizer_every_store_path(pkg, P, A, O):
     """The fused normaliser (MARLNAV_WRITE_OBS_NORM, utils.py:519-532) in
     every store path: the env-block kernel's per-thread-feature path (A3/O3
     full blocks), its generic path (A3/O8: D does not divide the block), the
-    pair-split kernel (LPR 8 at 60 envs, A16/O32): the fused output equals
+    draw-wave instantiation (at most one block per CU: 16384 full blocks, and
+    16001 whose ragged last block takes the generic path, whose barrier the
+    draw wave must meet), the pair-split kernel (LPR 8 at 60 envs, A16/O32):
+    the fused output equals
     (obs - mean) / scale in torch bit for bit, with a mean and scale per
     feature (re-inits included: 4-step episodes)."""
     from types import SimpleNamespace
