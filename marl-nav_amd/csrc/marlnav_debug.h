@@ -174,3 +174,10 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_PACKED_SPLIT
 #define MARLNAV_PACKED_SPLIT 0
 #endif
+// Env-block kernel, full step blocks: one barrier before the observation,
+// each wave moving its agent from its own gathered rows while the block's
+// spans are in flight (1; kOneStage in kernel_block.h), or a stage barrier
+// and a move barrier (0)
+#ifndef MARLNAV_ONE_STAGE
+#define MARLNAV_ONE_STAGE 0
+#endif
