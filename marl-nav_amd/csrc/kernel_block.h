@@ -73,31 +73,7 @@ struct BlockSpans {
             if (K[i] % A == w && (i != N - 1 || formation)) n += glds_count(NB[i]);
         return n;
     }
-    // One-stage blocks (kOneStage): no states span (each wave gathers its own
-    // agent's rows), the other spans re-spread over the waves (span i by
-    // wave K1[i] % A; K1[0] unused)
-    static constexpr int K1[N] = {-1, 0, 1, 2, 4, 5};
-    static constexpr int after_own(int w, bool formation)
-    {
-        int n = 0;
-        for (int i = 1; i < N; ++i)
-            if (K1[i] % A == w && (i != N - 1 || formation)) n += glds_count(NB[i]);
-        return n;
-    }
 };
-
-// One stage barrier (MARLNAV_ONE_STAGE): in a full step block each wave
-// gathers its own agent's 64 state rows and actions by LDS-DMA (one dword per
-// lane per instruction, into a per-wave transposed slice aliasing the
-// observation rows, which nothing writes before the observe phase), waits
-// for those alone, and moves its agent while the block's other spans are in
-// flight; the moved rows go to the states slice, which no LDS-DMA writes in
-// this mode, and the block meets ONE barrier before the observation instead
-// of a stage barrier and a move barrier. Every wave then checks the whole
-// block's obstacle and target coordinates itself (the coordinate check was
-// spread over the block's threads between the two barriers).
-template <int A, int O, bool OBS_ONLY>
-constexpr bool kOneStage = MARLNAV_ONE_STAGE && !OBS_ONLY;
 
 // plain strided copy of n elements by the block's NT threads (partial block)
 template <class T>
@@ -262,19 +238,8 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // evaluates the heading's sin/cos while the spans are still in flight,
     // not after the stage barrier
     float *actw = lds + BP::ACTW + 2 * E * (hw ? 0 : w);  // x at [l], y at [E + l]
-    // one-stage block (kOneStage; block-uniform)
-    const bool one = kOneStage<A, O, OBS_ONLY> && full;
-    // (one-stage) this wave's agent rows, transposed: component k of lane l
-    // at rowt[k * E + l]
-    float *rowt = lds + BP::OBS + 5 * E * (hw ? 0 : w);
     if (!OBS_ONLY && full && !hw) {
         const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
-        if (one) {
-            const float *ps = h_states + ((e0 + lane) * A + w) * 5;
-#pragma unroll
-            for (int k = 0; k < 5; ++k)
-                __builtin_amdgcn_global_load_lds(ps + k, (LdsVoid *)(rowt + k * E), 4, 0, 0);
-        }
         __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
         __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
     }
@@ -283,15 +248,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     static_assert(BS::NB[0] == R * 20 && BS::NB[1] == E * O * 8 && BS::NB[2] == E * 8 &&
                       BS::NB[3] == E * 4 && BS::NB[4] == E && BS::NB[5] == (5 * A + 2) * 4,
                   "span table and LDS plan agree");
-    static_assert(BP::R * BP::D >= 5 * BP::R, "the row slices fit the observation rows");
-    if (one) {
-        block_glds<BS::NB[1]>(BS::K1[1], A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
-        block_glds<BS::NB[2]>(BS::K1[2], A, w, b.target + e0 * 2, lds + BP::TG, lane);
-        block_glds<BS::NB[3]>(BS::K1[3], A, w, b.step_num + e0, lds + BP::SN, lane);
-        block_glds<BS::NB[4]>(BS::K1[4], A, w, b.terminates + e0, lds + BP::TM, lane);
-        if (b.formation)
-            block_glds<BS::NB[5]>(BS::K1[5], A, w, b.formation, lds + BP::FORM, lane);
-    } else if (full) {
+    if (full) {
         block_glds<BS::NB[0]>(BS::K[0], A, w, b.states + e0 * (A * 5), st, lane);
         block_glds<BS::NB[1]>(BS::K[1], A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
         block_glds<BS::NB[2]>(BS::K[2], A, w, b.target + e0 * 2, lds + BP::TG, lane);
@@ -373,15 +330,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // remaining staging latency
     float sn = 0.0f, c = 1.0f, a1 = 0.0f;
     if (!OBS_ONLY && !hw) {
-        if (one) {
-            // (one-stage: the span instructions this wave issued after its
-            // own rows and actions)
-            int n = 0;
-#pragma unroll
-            for (int ww = 0; ww < A; ++ww)
-                if (w == ww) n = b.formation ? BS::after_own(ww, true) : BS::after_own(ww, false);
-            wait_vmcnt(n);
-        } else if (full) {
+        if (full) {
             // span instructions this wave issued after its two action loads
             // (BlockSpans: the same table as the issue sites above)
             int n = 0;
@@ -409,62 +358,23 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     const bool row_on = l < ne && !hw;
     const int nrow = ne * A;
     int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
-    // (one-stage) wave w's moved rows off the fast range: bad_word[w]
-    float ox, oy, dx, dy;
-    if (one && !hw) {
-        // ---- _move_agents (environment.py:113-123) of this wave's agent,
-        // before the block's one barrier: its rows and actions landed above
-        ox = rowt[l];
-        oy = rowt[E + l];
-        dx = rowt[2 * E + l];
-        dy = rowt[3 * E + l];
-        const float spd = rowt[4 * E + l];
-        const float ndx = c * dx + (-sn) * dy;
-        const float ndy = sn * dx + c * dy;
-        const float v = clamp_t(spd + clamp_t(a1, pr.min_accel, pr.max_accel), pr.min_speed,
-                                pr.max_speed);
-        ox = ox + ndx * v;
-        oy = oy + ndy * v;
-        dx = ndx;
-        dy = ndy;
-        float *s = st + 5 * r;
-        s[0] = ox;
-        s[1] = oy;
-        s[2] = dx;
-        s[3] = dy;
-        s[4] = v;
-        CoordRange cm;
-        cm.add(ox);
-        cm.add(oy);
-        const bool bad = __ballot(!cm.ok()) != 0ull;
-        if (lane == 0) bad_word[w] = bad ? 1 : 0;
-    } else if (!one && tid == 0) {
-        *bad_word = 0;
-    }
+    if (tid == 0) *bad_word = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
     STAMPS_S(2);  // (substamps: every span this wave issued landed)
     __syncthreads();
     STAMP(1);
     if (MARLNAV_AB & 8192) {  // (AB 8192: timing / census only - staged, then exit;
-        asm volatile("" ::"v"(sn), "v"(c), "v"(a1), "v"(ox));  // the sin/cos kept alive)
+        asm volatile("" ::"v"(sn), "v"(c), "v"(a1));  // the sin/cos kept alive)
         return;
     }
 
     // obstacle and target coordinates of the block for the pair-math choice
     // (below); read before the move writes LDS, so the reads overlap it
-    // (a partial last block takes the IEEE path without checking). One-stage
-    // blocks: every wave checks all of them (no barrier follows to combine
-    // the waves' checks).
+    // (a partial last block takes the IEEE path without checking)
     CoordRange crange;
-    constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
-    static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
-    if (one && !hw) {
-#pragma unroll
-        for (int k2 = 0; k2 * 64 < NC; ++k2) {
-            const int i = l + k2 * 64;
-            if ((k2 + 1) * 64 <= NC || i < NC) crange.add(lds[BP::OB + i]);
-        }
-    } else if (full && !hw) {
+    if (full && !hw) {
+        constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
+        static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
 #pragma unroll
         for (int k2 = 0; k2 * NT < NC; ++k2) {
             const int i = tid + k2 * NT;
@@ -472,58 +382,49 @@ __global__ void __launch_bounds__(64 * (A + HELP))
         }
     }
 
-    if (!one) {
-        // ---- _move_agents (environment.py:113-123), own row in registers
-        {
-            const float *s = st + 5 * r;
-            ox = s[0];
-            oy = s[1];
-            dx = s[2];
-            dy = s[3];
-        }
-        if (!OBS_ONLY) {
-            const float ndx = c * dx + (-sn) * dy;
-            const float ndy = sn * dx + c * dy;
-            float *s = st + 5 * r;
-            const float v = clamp_t(s[4] + clamp_t(a1, pr.min_accel, pr.max_accel), pr.min_speed,
-                                    pr.max_speed);
-            ox = ox + ndx * v;
-            oy = oy + ndy * v;
-            dx = ndx;
-            dy = ndy;
-            if (row_on) {
-                s[0] = ox;
-                s[1] = oy;
-                s[2] = dx;
-                s[3] = dy;
-                s[4] = v;
-            }
-        }
-        // block-uniform choice of the pair math: the short sqrt / shared-
-        // reciprocal division (equal to IEEE there) when every coordinate of the
-        // block (obstacles and targets above, moved agents here) passes coord_ok,
-        // IEEE otherwise
-        if (full && !hw) {
-            crange.add(ox);
-            crange.add(oy);
-            // one word for the block, written only by waves that found one (all
-            // write 1: a benign race); read once after the barrier
-            const bool bad = __ballot(!crange.ok()) != 0ull;
-            if (lane == 0 && bad) *bad_word = 1;
-        }
-        __syncthreads();
+    // ---- _move_agents (environment.py:113-123), own row in registers
+    float ox, oy, dx, dy;
+    {
+        const float *s = st + 5 * r;
+        ox = s[0];
+        oy = s[1];
+        dx = s[2];
+        dy = s[3];
     }
+    if (!OBS_ONLY) {
+        const float ndx = c * dx + (-sn) * dy;
+        const float ndy = sn * dx + c * dy;
+        float *s = st + 5 * r;
+        const float v = clamp_t(s[4] + clamp_t(a1, pr.min_accel, pr.max_accel), pr.min_speed,
+                                pr.max_speed);
+        ox = ox + ndx * v;
+        oy = oy + ndy * v;
+        dx = ndx;
+        dy = ndy;
+        if (row_on) {
+            s[0] = ox;
+            s[1] = oy;
+            s[2] = dx;
+            s[3] = dy;
+            s[4] = v;
+        }
+    }
+    // block-uniform choice of the pair math: the short sqrt / shared-
+    // reciprocal division (equal to IEEE there) when every coordinate of the
+    // block (obstacles and targets above, moved agents here) passes coord_ok,
+    // IEEE otherwise
+    if (full && !hw) {
+        crange.add(ox);
+        crange.add(oy);
+        // one word for the block, written only by waves that found one (all
+        // write 1: a benign race); read once after the barrier
+        const bool bad = __ballot(!crange.ok()) != 0ull;
+        if (lane == 0 && bad) *bad_word = 1;
+    }
+    __syncthreads();
     STAMP(2);
     // the moved states are final except in finished envs (re-stored below)
-    bool fast;
-    if (one) {
-        bool bad = __ballot(!crange.ok()) != 0ull;
-#pragma unroll
-        for (int ww = 0; ww < A; ++ww) bad = bad || bad_word[ww] != 0;
-        fast = !bad;
-    } else {
-        fast = full && *bad_word == 0;
-    }
+    const bool fast = full && *bad_word == 0;
 
     // ---- observations of the moved state + reward terms (:99-100)
     float4 *red = reinterpret_cast<float4 *>(lds + BP::RED);

@@ -146,6 +146,10 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // MARLNAV_DEFER_BLOCK_ENV_OUT, MARLNAV_TAIL_PRIO (env-block kernel);
 // MARLNAV_SPLIT_OVERLAP, MARLNAV_SPLIT_OWN_ENV, MARLNAV_SPLIT_DEFER_ENV_OUT,
 // MARLNAV_SPLIT_ENV_PRIO (split kernel); MARLNAV_DEFER_REINIT_OUT (re-init).
+// Round 6 (HISTORY.md; code in git history at 9a7feb1): MARLNAV_ONE_STAGE
+// (each wave gathers its agent's rows by per-lane dword LDS-DMA and moves it
+// before ONE barrier: bit-exact, slower at every shape, 65536x3x3 6.55 ->
+// 6.89 us, 16384x3x3 4.65 -> 4.73, 2^20 envs 68.7 -> 74.4).
 // Round 5 (DESIGN.md §5 "Round 5"; code in git history at deae14b):
 // MARLNAV_BLOCK_ENV_ROT / MARLNAV_SPLIT_ENV_ROT (the per-env phase on wave
 // block % A / workgroup % 4: no gain, and the general re-init thread index
@@ -173,11 +177,4 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // (profiles/r06_ab_packed_split.txt): off (A/B builds: 1)
 #ifndef MARLNAV_PACKED_SPLIT
 #define MARLNAV_PACKED_SPLIT 0
-#endif
-// Env-block kernel, full step blocks: one barrier before the observation,
-// each wave moving its agent from its own gathered rows while the block's
-// spans are in flight (1; kOneStage in kernel_block.h), or a stage barrier
-// and a move barrier (0)
-#ifndef MARLNAV_ONE_STAGE
-#define MARLNAV_ONE_STAGE 0
 #endif
