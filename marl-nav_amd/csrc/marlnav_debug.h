@@ -178,3 +178,33 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_PACKED_SPLIT
 #define MARLNAV_PACKED_SPLIT 0
 #endif
+// Env-block kernel, pair-split instantiation (block_kernel PS: two waves
+// per agent, the row's target/obstacle pairs and its other-agent pairs on
+// different waves): 1 for the draw-wave grids (at most one block per CU),
+// 2 for every grid (A/B builds), 0 off
+#ifndef MARLNAV_PAIR_SPLIT
+#define MARLNAV_PAIR_SPLIT 0
+#endif
+// Env-block kernel: cache-policy bits of the staging LDS-DMA loads (actions
+// and spans; 0: default; A/B builds: 1 sc0, 2 nt, 16 sc1)
+#ifndef MARLNAV_STAGE_AUX
+#define MARLNAV_STAGE_AUX 0
+#endif
+// Env-block kernel stagger (A/B builds, timing only; 0 in the product): the
+// blocks with (blockIdx / DIV) % MOD >= MOD - N sleep MARLNAV_STAGGER x 64
+// cycles before issuing any load, so the other blocks of their CU stage,
+// compute and store ahead of them (burst overlap between co-resident blocks;
+// VERDICT r5 item 3). At 1024 blocks dealt round-robin over 8 XCDs of 32 CUs,
+// blockIdx >> 8 is the block's slot on its CU.
+#ifndef MARLNAV_STAGGER
+#define MARLNAV_STAGGER 0
+#endif
+#ifndef MARLNAV_STAGGER_DIV
+#define MARLNAV_STAGGER_DIV 256
+#endif
+#ifndef MARLNAV_STAGGER_MOD
+#define MARLNAV_STAGGER_MOD 4
+#endif
+#ifndef MARLNAV_STAGGER_N
+#define MARLNAV_STAGGER_N 1
+#endif
