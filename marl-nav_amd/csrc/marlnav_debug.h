@@ -190,6 +190,15 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #ifndef MARLNAV_STAGE_AUX
 #define MARLNAV_STAGE_AUX 0
 #endif
+// Split kernel (A/B builds, timing only): every workgroup makes one
+// returning atomic on a per-XCD counter after its stores - the claim a
+// cross-workgroup finished-env work list would cost (kernel_split.h)
+#ifndef MARLNAV_CLAIM_PROBE
+#define MARLNAV_CLAIM_PROBE 0
+#endif
+#if MARLNAV_CLAIM_PROBE
+__device__ unsigned g_claim_probe[8 * 32];
+#endif
 // Env-block kernel stagger (A/B builds, timing only; 0 in the product): the
 // blocks with (blockIdx / DIV) % MOD >= MOD - N sleep MARLNAV_STAGGER x 64
 // cycles before issuing any load, so the other blocks of their CU stage,
