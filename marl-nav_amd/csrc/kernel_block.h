@@ -363,6 +363,12 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP))
         __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, MARLNAV_STAGE_AUX);
         __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, MARLNAV_STAGE_AUX);
     }
+#if MARLNAV_ACT_FIRST
+    // (A/B builds) every wave's action loads issued before any span: the
+    // CU's memory pipe returns them first, so the heading's sin/cos runs
+    // under the spans' flight
+    __syncthreads();
+#endif
     // ---- stage the block (spans spread over the waves: span k by wave k % A)
     using BS = BlockSpans<A, O, PS>;
     static_assert(BS::NB[0] == R * 20 && BS::NB[1] == E * O * 8 && BS::NB[2] == E * 8 &&
@@ -598,6 +604,16 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP))
         lds_row_write<D>(obs_rows + r * D, rowv);
         if (!OBS_ONLY) red[r] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
     }
+    // (MARLNAV_CNT_EARLY, A/B builds: wave 0's counter pointer and slot
+    // count read before the observe barrier, off the per-env chain)
+    uint64_t *cnt_e = nullptr;
+    int64_t slots_e = 0;
+    if (MARLNAV_CNT_EARLY && !OBS_ONLY && w == 0) {
+        KArgsK *kl = kargs_late<kHotKargsOff>();
+        cnt_e = kl->a.b.counters;
+        slots_e = kl->a.waves;
+        asm volatile("" ::"s"(cnt_e), "s"(slots_e));
+    }
     __syncthreads();
     STAMP(3);
     if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
@@ -719,8 +735,8 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP))
                 flg[0] = (int)__popcll(finmask);
                 if ((c_trunc | c_col | c_tar) && !(MARLNAV_AB & 512)) {  // (AB 512: timing only)
                     KArgsK *kl = kargs_late<kHotKargsOff>();
-                    uint64_t *cnt = kl->a.b.counters;
-                    const int64_t slots = kl->a.waves;
+                    uint64_t *cnt = MARLNAV_CNT_EARLY ? cnt_e : kl->a.b.counters;
+                    const int64_t slots = MARLNAV_CNT_EARLY ? slots_e : kl->a.waves;
                     if (cnt) {
                         const int64_t sl = blk < slots ? blk : blk % slots;
                         if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);

@@ -199,6 +199,14 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 #if MARLNAV_CLAIM_PROBE
 __device__ unsigned g_claim_probe[8 * 32];
 #endif
+// Env-block kernel (A/B builds): a block barrier between the waves' action
+// loads and the spans' LDS-DMA (kernel_block.h)
+#ifndef MARLNAV_ACT_FIRST
+#define MARLNAV_ACT_FIRST 0
+#endif
+#ifndef MARLNAV_CNT_EARLY
+#define MARLNAV_CNT_EARLY 0
+#endif
 // Env-block kernel stagger (A/B builds, timing only; 0 in the product): the
 // blocks with (blockIdx / DIV) % MOD >= MOD - N sleep MARLNAV_STAGGER x 64
 // cycles before issuing any load, so the other blocks of their CU stage,
