@@ -301,8 +301,11 @@ constexpr bool kBlockEarlyOut = MARLNAV_EARLY_OUT < 0 ? O >= 8 : MARLNAV_EARLY_O
 // summed through the bond term, waves A..2A-1 read the moved row after the
 // move barrier and compute its obstacle pairs, so each wave's observation
 // chain is about half as long; wave 0 adds the risk term (row_half_sum).
-template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false, bool PS = false>
-__global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP))
+// T > 1 (A/B builds, MARLNAV_BLOCK_TILES): T consecutive env blocks per
+// workgroup, each with its own LDS region and A waves, meeting the same
+// barriers (fewer, larger workgroups to dispatch).
+template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false, bool PS = false, int T = 1>
+__global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
     block_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
                  const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
                  int64_t h_P, KArgs k)
@@ -315,8 +318,12 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP))
     static_assert(!HELP || (!OBS_ONLY && !NOISY), "the draw wave serves the native re-init step");
     static_assert(!PS || (!OBS_ONLY && !NOISY && D % 4 == 0 && (2 + 2 * O) % 4 == 0),
                   "pair split: the native step, 16-byte aligned half rows");
+    static_assert(T == 1 || (!PS && !HELP && BP::FLOATS % 4 == 0), "tiles per workgroup: plain blocks");
     (void)k;  // read through kargs_late<kHotKargsOff>()
-    extern __shared__ __attribute__((aligned(16))) float lds[];
+    extern __shared__ __attribute__((aligned(16))) float lds_wg[];
+    // (T > 1: this wave's env block within the workgroup)
+    const int sb = T > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) / NWA : 0;
+    float *lds = lds_wg + sb * BP::FLOATS;
 #if MARLNAV_STAMPS
     unsigned long long t_entry;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
@@ -327,13 +334,13 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP))
         MARLNAV_STAGGER_MOD - MARLNAV_STAGGER_N)
         __builtin_amdgcn_s_sleep(MARLNAV_STAGGER);
 #endif
-    const int tid = (int)threadIdx.x;
+    const int tid = (int)threadIdx.x - sb * NWA * 64;
     const unsigned lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // agent of this wave
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) - sb * NWA;  // agent of this wave
     const bool hw = HELP && w == NWA;  // the draw wave (no agent)
     const bool h1 = PS && w >= A && !hw;  // PS: the other-agent half of agent w - A
     const int wa = PS && w >= A ? w - A : w;  // agent of this wave
-    const int64_t blk = blockIdx.x;
+    const int64_t blk = (int64_t)blockIdx.x * T + sb;  // env block
     const int64_t gw = blk * (NWA + HELP) + w;  // stamps slot
     KArgsK *K = kargs_late<kHotKargsOff>();
     const int64_t P = h_P;
@@ -349,7 +356,7 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP))
     STAMP(0);
     float *st = lds + BP::ST;
     const int64_t e0 = blk * E;
-    const int ne = (int)((P - e0) < E ? (P - e0) : E);
+    const int ne = (int)((P - e0) < E ? ((P - e0) > 0 ? (P - e0) : 0) : E);
     const bool full = ne == E;
 
     // ---- this wave's actions (lane l: agent w of env l) into its own LDS

@@ -207,6 +207,11 @@ __device__ unsigned g_claim_probe[8 * 32];
 #ifndef MARLNAV_CNT_EARLY
 #define MARLNAV_CNT_EARLY 0
 #endif
+// Env-block kernel (A/B builds): env blocks per workgroup of the step kernel
+// at grids above the draw-wave size (1: one, the product)
+#ifndef MARLNAV_BLOCK_TILES
+#define MARLNAV_BLOCK_TILES 1
+#endif
 // Env-block kernel stagger (A/B builds, timing only; 0 in the product): the
 // blocks with (blockIdx / DIV) % MOD >= MOD - N sleep MARLNAV_STAGGER x 64
 // cycles before issuing any load, so the other blocks of their CU stage,
