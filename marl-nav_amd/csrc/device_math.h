@@ -1064,33 +1064,22 @@ __device__ __forceinline__ float bond_term(float d, const MarlnavParams &pr, boo
 }
 
 // The per-agent reward of _rews_and_terms (environment.py:184-269) for one
-// row, in three parts so that the pair-split block kernel can evaluate the
-// target terms and the agent-band terms on different waves and sum them
-// later: row_terms_target (heading term :253-257, soft term :240-241),
-// row_terms_band (distance-band term :243-251, bond mean :259-269) and
-// row_reward_sum (the sum in the reference's order, :223-233).
-template <bool FAST, bool REFC>
-__device__ __forceinline__ void row_terms_target(float ta, float td, const MarlnavParams &pr,
-                                                 bool &ok, float &head, float &soft)
+// row, from its target bearing/distance, risk and collision flags, the count
+// of others in the distance band and the torch-order sum of bond terms.
+template <int A, bool FAST, bool REFC>
+__device__ __forceinline__ RowOut row_reward(float ta, float td, bool risk_any, bool col_any,
+                                             float band, float bond, const MarlnavParams &pr,
+                                             bool &ok)
 {
-    head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+    const float head = fabsf(ta) < pr.max_angle_diff ? 1.0f : 0.0f;
+    const float bandc = band < pr.max_at_prop_d ? band : pr.max_at_prop_d;
+    float dsc, soft;
     if (FAST && (pr.flags & kTermsFastFlag)) {
         // exact: the host set kTermsFastFlag only for parameters inside the
         // div_c / recip_fast guards (terms_fast_params), and FAST coordinates
         // bound every distance (coord_ok), so every operand stays in range
         const DivC d_init = make_divc(pr.init_dist, ok);
         soft = -1.0f * div_c(td, d_init, ok);
-    } else {
-        soft = -1.0f * (td / pr.init_dist);
-    }
-}
-
-template <int A, bool FAST, bool REFC>
-__device__ __forceinline__ void row_terms_band(float band, float bond, const MarlnavParams &pr,
-                                               bool &ok, float &dsc, float &bondm)
-{
-    const float bandc = band < pr.max_at_prop_d ? band : pr.max_at_prop_d;
-    if (FAST && (pr.flags & kTermsFastFlag)) {
         if constexpr (REFC) {
             dsc = bandc * 0.5f;
         } else {
@@ -1099,53 +1088,20 @@ __device__ __forceinline__ void row_terms_band(float band, float bond, const Mar
         }
     } else {
         dsc = bandc / pr.max_at_prop_d;
+        soft = -1.0f * (td / pr.init_dist);
     }
-    bondm = bond / (float)(A - 1);  // the bond sum can be tiny: IEEE
-}
-
-// the sum through the bond term (the reference's order, :223-231) ...
-__device__ __forceinline__ void row_reward_sum4(float head, float dsc, float soft, float bondm,
-                                                const MarlnavParams &pr, float &rm, float &rh)
-{
-    rm = pr.target_factor * 0.0f + pr.heading_factor * head;
-    rh = pr.target_factor * 1.0f + pr.heading_factor * head;
+    const float bondm = bond / (float)(A - 1);  // the bond sum can be tiny: IEEE
+    const float risk = risk_any ? 1.0f : 0.0f;
+    float rm = pr.target_factor * 0.0f + pr.heading_factor * head;
+    float rh = pr.target_factor * 1.0f + pr.heading_factor * head;
     rm = rm + pr.distance_factor * dsc;
     rh = rh + pr.distance_factor * dsc;
     rm = rm + pr.soft_factor * soft;
     rh = rh + pr.soft_factor * soft;
     rm = rm + pr.bond_factor * bondm;
     rh = rh + pr.bond_factor * bondm;
-}
-
-// ... and its last term, the risk penalty (:232-233)
-__device__ __forceinline__ void row_reward_risk(bool risk_any, const MarlnavParams &pr, float &rm,
-                                                float &rh)
-{
-    const float risk = risk_any ? 1.0f : 0.0f;
     rm = rm - pr.risk_factor * risk;
     rh = rh - pr.risk_factor * risk;
-}
-
-__device__ __forceinline__ void row_reward_sum(float head, float dsc, float soft, float bondm,
-                                               bool risk_any, const MarlnavParams &pr, float &rm,
-                                               float &rh)
-{
-    row_reward_sum4(head, dsc, soft, bondm, pr, rm, rh);
-    row_reward_risk(risk_any, pr, rm, rh);
-}
-
-// The three parts for one row: target bearing/distance, risk and collision
-// flags, the count of others in the distance band and the torch-order sum of
-// bond terms.
-template <int A, bool FAST, bool REFC>
-__device__ __forceinline__ RowOut row_reward(float ta, float td, bool risk_any, bool col_any,
-                                             float band, float bond, const MarlnavParams &pr,
-                                             bool &ok)
-{
-    float head, soft, dsc, bondm, rm, rh;
-    row_terms_target<FAST, REFC>(ta, td, pr, ok, head, soft);
-    row_terms_band<A, FAST, REFC>(band, bond, pr, ok, dsc, bondm);
-    row_reward_sum(head, dsc, soft, bondm, risk_any, pr, rm, rh);
     return RowOut{rm, rh, (col_any ? 1u : 0u) | ((td < pr.target_radius) ? 2u : 0u)};
 }
 

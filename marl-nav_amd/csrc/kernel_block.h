@@ -17,12 +17,10 @@
 // packed observation rows are assembled in LDS and streamed out as one
 // contiguous span (a store instruction covers 1 KiB, 8 cache lines, where
 // register-row stores at a 48-byte lane stride touch 24).
-template <int A, int O, int H = 1>
+template <int A, int O>
 struct BlockPlan {
-    // H = 2: the pair-split instantiation (block_kernel PS) - two waves per
-    // agent, each with half of the row's pairs and its own reward-term slots
     static constexpr int E = 64, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
-    static constexpr int NT = 64 * A * H;                  // threads per block (agent waves)
+    static constexpr int NT = 64 * A;                      // threads per block
     static constexpr int ST = 0;                           // (R, 5)
     static constexpr int ACTW = (ST + R * 5 + 3) & ~3;     // (A, 2, E) actions, per wave
     static constexpr int OB = (ACTW + 2 * R + 3) & ~3;     // (E, O, 2)
@@ -30,23 +28,22 @@ struct BlockPlan {
     static constexpr int SN = (TG + E * 2 + 3) & ~3;       // (E,)
     static constexpr int TM = (SN + E + 3) & ~3;           // (E,) bytes
     static constexpr int FORM = (TM + E / 4 + 3) & ~3;     // 5A + 2 (native re-init)
-    static constexpr int RED = (FORM + 5 * A + 2 + 3) & ~3;  // (H, R, 4) reward terms
-    static constexpr int OBS = RED + 4 * R * H;            // (R, D) packed rows
+    static constexpr int RED = (FORM + 5 * A + 2 + 3) & ~3;  // (R, 4) reward terms
+    static constexpr int OBS = RED + 4 * R;                // (R, D) packed rows
     static constexpr int LIST = (OBS + R * D + 3) & ~3;    // (E,) finished envs
     static constexpr int FLG = LIST + E;                   // [0] nfin, [1 + w] wave w coords bad
     static constexpr int FRESH = (FLG + 1 + A + 3) & ~3;   // (2O, E) fresh obstacle draws
     static constexpr int FLOATS = FRESH + 2 * O * E;
     static_assert(A >= 2 && A <= 16, "one wave per agent");
-    static_assert(H == 1 || H == 2, "one or two waves per agent");
 };
 
 // Copy NB bytes of the block's span k into LDS by LDS-DMA from the wave
 // k % A (spans spread over the block's waves).
 template <int NB, int AUX = 0>
 __device__ __forceinline__ void block_glds(int k, int A, int w, const void *src, float *dst,
-                                           unsigned lane, bool ps = false)
+                                           unsigned lane)
 {
-    if ((ps ? A + k % A : k % A) == w) glds_span<NB, AUX>(src, dst, lane);
+    if (k % A == w) glds_span<NB, AUX>(src, dst, lane);
 }
 
 // LDS-DMA instructions glds_span<NB> issues (one per KiB, one for the tail)
@@ -58,10 +55,7 @@ __host__ __device__ constexpr int glds_count(int NB)
 // The staging spans of a full block, in issue order: span id k (issued by
 // wave k % A) and its byte count. The issue sites and the per-wave vmcnt
 // that lets each wave use its own actions early both read this one table.
-// PS (pair-split instantiation): the spans go to the second wave of each
-// agent (A + k % A), which loads no actions; the first waves issue only
-// their action loads.
-template <int A, int O, bool PS = false>
+template <int A, int O>
 struct BlockSpans {
     using BP = BlockPlan<A, O>;
     static constexpr int N = 6;
@@ -76,109 +70,10 @@ struct BlockSpans {
     {
         int n = 0;
         for (int i = 0; i < N; ++i)
-            if ((PS ? A + K[i] % A : K[i] % A) == w && (i != N - 1 || formation))
-                n += glds_count(NB[i]);
+            if (K[i] % A == w && (i != N - 1 || formation)) n += glds_count(NB[i]);
         return n;
     }
 };
-
-// The pair-split block kernel's two halves of a row (block_kernel PS, FAST
-// coordinates, TERMS): the same pair math (pairs_fast) and the same reward
-// parts as observe_row_own, split by pair kind. Half 0 - the target and the
-// A - 1 other agents - writes columns [0, 2) and [2 + 2O, D) of the packed
-// row and returns (rm, rh, bits, 0): the two rewards summed through the bond
-// term (row_reward_sum4); half 1 - the O obstacles - writes columns
-// [2, 2 + 2O) and returns (0, 0, bits, 0); bits: 1 collision, 2 in the target
-// radius, 4 risk. row_half_sum adds the risk term.
-template <int A, int O, bool REFC>
-__device__ __forceinline__ float4 observe_half_ta(const float *__restrict__ sts,
-                                                  const float *__restrict__ tge, int a, float ox,
-                                                  float oy, float dx, float dy,
-                                                  float *__restrict__ row, const MarlnavParams &pr)
-{
-    constexpr int NP = A;  // the target, then the others in row order
-    float px[NP], py[NP], pd[NP], pg[NP];
-    px[0] = tge[0];
-    py[0] = tge[1];
-#pragma unroll
-    for (int j = 0; j < A - 1; ++j) {
-        const int m = j + (j >= a ? 1 : 0);
-        px[1 + j] = sts[5 * m];
-        py[1 + j] = sts[5 * m + 1];
-    }
-    pairs_fast<NP>(ox, oy, dx, dy, px, py, pr.cap_distance, pd, pg);
-    float rowt[2], rowa[2 * (A - 1)];
-    rowt[0] = pg[0];
-    rowt[1] = pd[0];
-    bool ag_risk = false, ag_col = false;
-    float band = 0.0f;
-#pragma unroll
-    for (int j = 0; j < A - 1; ++j) {
-        const float d = pd[1 + j];
-        rowa[j] = pg[1 + j];
-        rowa[(A - 1) + j] = d;
-        ag_risk |= d < pr.ag_risk_dist;
-        ag_col |= d < pr.ag_coll_dist;
-        band += (pr.agents_min_d < d && d < pr.agents_max_d) ? 1.0f : 0.0f;
-    }
-    lds_row_write<2>(row, rowt);
-    lds_row_write<2 * (A - 1)>(row + 2 + 2 * O, rowa);
-    bool ok = true;
-    float bond;
-    if (pr.flags & kTermsFastFlag)
-        bond = torch_row_sum_r<A - 1>(pd + 1, [&](float d) { return bond_term<true, REFC>(d, pr, ok); });
-    else
-        bond = torch_row_sum_r<A - 1>(pd + 1, [&](float d) { return bond_term<false>(d, pr, ok); });
-    float head, soft, dsc, bondm, rm, rh;
-    row_terms_target<true, REFC>(pg[0], pd[0], pr, ok, head, soft);
-    row_terms_band<A, true, REFC>(band, bond, pr, ok, dsc, bondm);
-    row_reward_sum4(head, dsc, soft, bondm, pr, rm, rh);
-    const unsigned bits = (ag_col ? 1u : 0u) | ((pd[0] < pr.target_radius) ? 2u : 0u) |
-                          (ag_risk ? 4u : 0u);
-    return make_float4(rm, rh, __uint_as_float(bits), 0.0f);
-}
-
-template <int A, int O>
-__device__ __forceinline__ float4 observe_half_ob(const float *__restrict__ obe, float ox,
-                                                  float oy, float dx, float dy,
-                                                  float *__restrict__ row, const MarlnavParams &pr)
-{
-    float px[O], py[O], pd[O], pg[O];
-#pragma unroll
-    for (int j = 0; j < O; ++j) {
-        px[j] = obe[2 * j];
-        py[j] = obe[2 * j + 1];
-    }
-    pairs_fast<O>(ox, oy, dx, dy, px, py, pr.cap_distance, pd, pg);
-    float rowv[2 * O];
-    bool ob_risk = false, ob_col = false;
-#pragma unroll
-    for (int j = 0; j < O; ++j) {
-        rowv[j] = pg[j];
-        rowv[O + j] = pd[j];
-        ob_risk |= pd[j] < pr.ob_risk_dist;
-        ob_col |= pd[j] < pr.ob_coll_dist;
-    }
-    lds_row_write<2 * O>(row + 2, rowv);
-    const unsigned bits = (ob_col ? 1u : 0u) | (ob_risk ? 4u : 0u);
-    return make_float4(0.0f, 0.0f, __uint_as_float(bits), 0.0f);
-}
-
-// the row's RowOut from the two halves' terms (observe_half_ta / _ob)
-__device__ __forceinline__ RowOut row_half_sum(float4 h0, float z1, const MarlnavParams &pr)
-{
-    const unsigned b0 = __float_as_uint(h0.z), b1 = __float_as_uint(z1);
-    float rm = h0.x, rh = h0.y;
-    row_reward_risk(((b0 | b1) & 4u) != 0u, pr, rm, rh);
-    return RowOut{rm, rh, ((b0 | b1) & 1u) | (b0 & 2u)};
-}
-
-// the row's RowOut.flags word from the halves' bits
-__device__ __forceinline__ unsigned row_half_flags(float z0, float z1)
-{
-    const unsigned b0 = __float_as_uint(z0), b1 = __float_as_uint(z1);
-    return ((b0 | b1) & 1u) | (b0 & 2u);
-}
 
 // plain strided copy of n elements by the block's NT threads (partial block)
 template <class T>
@@ -295,53 +190,31 @@ constexpr bool kBlockEarlyOut = MARLNAV_EARLY_OUT < 0 ? O >= 8 : MARLNAV_EARLY_O
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
 // re-init; none in most blocks) | rows and states stream out of LDS.
-// PS (pair-split instantiation, grids of at most one block per CU): two
-// waves per agent on the SIMDs such a grid leaves idle - waves 0..A-1 move
-// their agent and compute its target and other-agent pairs with the reward
-// summed through the bond term, waves A..2A-1 read the moved row after the
-// move barrier and compute its obstacle pairs, so each wave's observation
-// chain is about half as long; wave 0 adds the risk term (row_half_sum).
-// T > 1 (A/B builds, MARLNAV_BLOCK_TILES): T consecutive env blocks per
-// workgroup, each with its own LDS region and A waves, meeting the same
-// barriers (fewer, larger workgroups to dispatch).
-template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false, bool PS = false, int T = 1>
-__global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
+template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false>
+__global__ void __launch_bounds__(64 * (A + HELP))
     block_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
                  const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
                  int64_t h_P, KArgs k)
 {
-    using BP = BlockPlan<A, O, PS ? 2 : 1>;
+    using BP = BlockPlan<A, O>;
     // NT: the agent waves' threads, over which every work loop is spread
-    // (HELP: one more wave, w == NWA, draws the fresh obstacles and otherwise
+    // (HELP: one more wave, w == A, draws the fresh obstacles and otherwise
     // only meets the barriers)
-    constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT, NWA = A * (PS ? 2 : 1);
+    constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
     static_assert(!HELP || (!OBS_ONLY && !NOISY), "the draw wave serves the native re-init step");
-    static_assert(!PS || (!OBS_ONLY && !NOISY && D % 4 == 0 && (2 + 2 * O) % 4 == 0),
-                  "pair split: the native step, 16-byte aligned half rows");
-    static_assert(T == 1 || (!PS && !HELP && BP::FLOATS % 4 == 0), "tiles per workgroup: plain blocks");
     (void)k;  // read through kargs_late<kHotKargsOff>()
-    extern __shared__ __attribute__((aligned(16))) float lds_wg[];
-    // (T > 1: this wave's env block within the workgroup)
-    const int sb = T > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) / NWA : 0;
-    float *lds = lds_wg + sb * BP::FLOATS;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS
     unsigned long long t_entry;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
 #endif
     if (MARLNAV_AB & 4096) return;  // (AB 4096: timing only - the launch alone)
-#if MARLNAV_STAGGER
-    if (((int)blockIdx.x / MARLNAV_STAGGER_DIV) % MARLNAV_STAGGER_MOD >=
-        MARLNAV_STAGGER_MOD - MARLNAV_STAGGER_N)
-        __builtin_amdgcn_s_sleep(MARLNAV_STAGGER);
-#endif
-    const int tid = (int)threadIdx.x - sb * NWA * 64;
+    const int tid = (int)threadIdx.x;
     const unsigned lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) - sb * NWA;  // agent of this wave
-    const bool hw = HELP && w == NWA;  // the draw wave (no agent)
-    const bool h1 = PS && w >= A && !hw;  // PS: the other-agent half of agent w - A
-    const int wa = PS && w >= A ? w - A : w;  // agent of this wave
-    const int64_t blk = (int64_t)blockIdx.x * T + sb;  // env block
-    const int64_t gw = blk * (NWA + HELP) + w;  // stamps slot
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // agent of this wave
+    const bool hw = HELP && w == A;  // the draw wave (no agent)
+    const int64_t blk = blockIdx.x;
+    const int64_t gw = blk * (A + HELP) + w;  // stamps slot
     KArgsK *K = kargs_late<kHotKargsOff>();
     const int64_t P = h_P;
     // launch_block's grid is exactly ntiles blocks: no exit test. The staging
@@ -356,7 +229,7 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
     STAMP(0);
     float *st = lds + BP::ST;
     const int64_t e0 = blk * E;
-    const int ne = (int)((P - e0) < E ? ((P - e0) > 0 ? (P - e0) : 0) : E);
+    const int ne = (int)((P - e0) < E ? (P - e0) : E);
     const bool full = ne == E;
 
     // ---- this wave's actions (lane l: agent w of env l) into its own LDS
@@ -364,37 +237,31 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
     // them alone (vmcnt = the span instructions it issued after them) and
     // evaluates the heading's sin/cos while the spans are still in flight,
     // not after the stage barrier
-    float *actw = lds + BP::ACTW + 2 * E * (hw || h1 ? 0 : w);  // x at [l], y at [E + l]
-    if (!OBS_ONLY && full && !hw && !h1) {
+    float *actw = lds + BP::ACTW + 2 * E * (hw ? 0 : w);  // x at [l], y at [E + l]
+    if (!OBS_ONLY && full && !hw) {
         const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
-        __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, MARLNAV_STAGE_AUX);
-        __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, MARLNAV_STAGE_AUX);
+        __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
     }
-#if MARLNAV_ACT_FIRST
-    // (A/B builds) every wave's action loads issued before any span: the
-    // CU's memory pipe returns them first, so the heading's sin/cos runs
-    // under the spans' flight
-    __syncthreads();
-#endif
     // ---- stage the block (spans spread over the waves: span k by wave k % A)
-    using BS = BlockSpans<A, O, PS>;
+    using BS = BlockSpans<A, O>;
     static_assert(BS::NB[0] == R * 20 && BS::NB[1] == E * O * 8 && BS::NB[2] == E * 8 &&
                       BS::NB[3] == E * 4 && BS::NB[4] == E && BS::NB[5] == (5 * A + 2) * 4,
                   "span table and LDS plan agree");
     if (full) {
-        block_glds<BS::NB[0], MARLNAV_STAGE_AUX>(BS::K[0], A, w, b.states + e0 * (A * 5), st, lane, PS);
-        block_glds<BS::NB[1], MARLNAV_STAGE_AUX>(BS::K[1], A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane, PS);
-        block_glds<BS::NB[2], MARLNAV_STAGE_AUX>(BS::K[2], A, w, b.target + e0 * 2, lds + BP::TG, lane, PS);
+        block_glds<BS::NB[0]>(BS::K[0], A, w, b.states + e0 * (A * 5), st, lane);
+        block_glds<BS::NB[1]>(BS::K[1], A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
+        block_glds<BS::NB[2]>(BS::K[2], A, w, b.target + e0 * 2, lds + BP::TG, lane);
         if (!OBS_ONLY) {
-            block_glds<BS::NB[3], MARLNAV_STAGE_AUX>(BS::K[3], A, w, b.step_num + e0, lds + BP::SN, lane, PS);
-            block_glds<BS::NB[4], MARLNAV_STAGE_AUX>(BS::K[4], A, w, b.terminates + e0, lds + BP::TM, lane, PS);
+            block_glds<BS::NB[3]>(BS::K[3], A, w, b.step_num + e0, lds + BP::SN, lane);
+            block_glds<BS::NB[4]>(BS::K[4], A, w, b.terminates + e0, lds + BP::TM, lane);
             if (b.formation)
-                block_glds<BS::NB[5], MARLNAV_STAGE_AUX>(BS::K[5], A, w, b.formation, lds + BP::FORM, lane, PS);
+                block_glds<BS::NB[5]>(BS::K[5], A, w, b.formation, lds + BP::FORM, lane);
         }
     } else if (!hw) {
         const int nr = ne * A;
         block_copy(b.states + e0 * (A * 5), st, nr * 5, tid, NT);
-        if (!OBS_ONLY && !h1 && (int)lane < ne) {  // (each lane its own slots: no barrier)
+        if (!OBS_ONLY && (int)lane < ne) {  // (each lane its own slots: no barrier)
             const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
             actw[lane] = pa[0];
             actw[E + lane] = pa[1];
@@ -462,7 +329,7 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
     // the heading's sin/cos (environment.py:113-115, 131-137), under the
     // remaining staging latency
     float sn = 0.0f, c = 1.0f, a1 = 0.0f;
-    if (!OBS_ONLY && !hw && !h1) {
+    if (!OBS_ONLY && !hw) {
         if (full) {
             // span instructions this wave issued after its two action loads
             // (BlockSpans: the same table as the issue sites above)
@@ -487,7 +354,7 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
         STAMPS_S(1);  // (substamps: the heading's sin/cos done)
     }
     const int l = (int)lane;  // env of this lane within the block
-    const int r = l * A + (hw ? 0 : wa);  // row of this lane (the draw wave has none)
+    const int r = l * A + (hw ? 0 : w);  // row of this lane (the draw wave has none)
     const bool row_on = l < ne && !hw;
     const int nrow = ne * A;
     int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
@@ -516,15 +383,15 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
     }
 
     // ---- _move_agents (environment.py:113-123), own row in registers
-    float ox = 0.0f, oy = 0.0f, dx = 0.0f, dy = 0.0f;
-    if (!h1) {
+    float ox, oy, dx, dy;
+    {
         const float *s = st + 5 * r;
         ox = s[0];
         oy = s[1];
         dx = s[2];
         dy = s[3];
     }
-    if (!OBS_ONLY && !h1) {
+    if (!OBS_ONLY) {
         const float ndx = c * dx + (-sn) * dy;
         const float ndy = sn * dx + c * dy;
         float *s = st + 5 * r;
@@ -547,10 +414,8 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
     // block (obstacles and targets above, moved agents here) passes coord_ok,
     // IEEE otherwise
     if (full && !hw) {
-        if (!h1) {
-            crange.add(ox);
-            crange.add(oy);
-        }
+        crange.add(ox);
+        crange.add(oy);
         // one word for the block, written only by waves that found one (all
         // write 1: a benign race); read once after the barrier
         const bool bad = __ballot(!crange.ok()) != 0ull;
@@ -560,34 +425,11 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
     STAMP(2);
     // the moved states are final except in finished envs (re-stored below)
     const bool fast = full && *bad_word == 0;
-    if (h1 && row_on) {  // (PS: the moved own row, written by wave wa)
-        const float *s = st + 5 * r;
-        ox = s[0];
-        oy = s[1];
-        dx = s[2];
-        dy = s[3];
-    }
 
     // ---- observations of the moved state + reward terms (:99-100)
     float4 *red = reinterpret_cast<float4 *>(lds + BP::RED);
     float *obs_rows = lds + BP::OBS;
-    if (PS && row_on && __builtin_expect(fast, 1)) {
-        // the row's halves (observe_half_ta / observe_half_ob): columns and
-        // reward parts; wave 0 adds the risk term (row_half_sum)
-        float4 t;
-        const bool refc =
-            !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f && pr.max_at_prop_d == 2.0f;
-        if (h1)
-            t = observe_half_ob<A, O>(lds + BP::OB + 2 * O * l, ox, oy, dx, dy, obs_rows + r * D, pr);
-        else if (refc)
-            t = observe_half_ta<A, O, true>(st + 5 * A * l, lds + BP::TG + 2 * l, wa, ox, oy, dx,
-                                            dy, obs_rows + r * D, pr);
-        else
-            t = observe_half_ta<A, O, false>(st + 5 * A * l, lds + BP::TG + 2 * l, wa, ox, oy, dx,
-                                             dy, obs_rows + r * D, pr);
-        STAMPS_S(3);  // (substamps: this lane's row computed)
-        red[(h1 ? R : 0) + r] = t;
-    } else if (row_on && !h1) {
+    if (row_on) {
         float rowv[D];
         RowOut ro;
         bool unused = true;
@@ -610,16 +452,6 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
         STAMPS_S(3);  // (substamps: this lane's row computed)
         lds_row_write<D>(obs_rows + r * D, rowv);
         if (!OBS_ONLY) red[r] = make_float4(ro.r_miss, ro.r_hit, __uint_as_float(ro.flags), 0.0f);
-    }
-    // (MARLNAV_CNT_EARLY, A/B builds: wave 0's counter pointer and slot
-    // count read before the observe barrier, off the per-env chain)
-    uint64_t *cnt_e = nullptr;
-    int64_t slots_e = 0;
-    if (MARLNAV_CNT_EARLY && !OBS_ONLY && w == 0) {
-        KArgsK *kl = kargs_late<kHotKargsOff>();
-        cnt_e = kl->a.b.counters;
-        slots_e = kl->a.waves;
-        asm volatile("" ::"s"(cnt_e), "s"(slots_e));
     }
     __syncthreads();
     STAMP(3);
@@ -654,17 +486,10 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
                 unsigned rf[A];
 #pragma unroll
                 for (int i = 0; i < A; ++i) {
-                    if (PS && fast) {  // (the two halves' parts, in the reference's order)
-                        const RowOut t = row_half_sum(red[A * l + i], red[R + A * l + i].z, pr);
-                        rx[i] = t.r_miss;
-                        ry[i] = t.r_hit;
-                        rf[i] = t.flags;
-                    } else {
-                        const float4 t = red[A * l + i];
-                        rx[i] = t.x;
-                        ry[i] = t.y;
-                        rf[i] = __float_as_uint(t.z);
-                    }
+                    const float4 t = red[A * l + i];
+                    rx[i] = t.x;
+                    ry[i] = t.y;
+                    rf[i] = __float_as_uint(t.z);
                 }
                 const EnvEnd ee = env_end<A>([&](int i) { return rf[i]; }, lds[BP::SN + l],
                                              reinterpret_cast<const uint8_t *>(lds + BP::TM)[l],
@@ -742,8 +567,8 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
                 flg[0] = (int)__popcll(finmask);
                 if ((c_trunc | c_col | c_tar) && !(MARLNAV_AB & 512)) {  // (AB 512: timing only)
                     KArgsK *kl = kargs_late<kHotKargsOff>();
-                    uint64_t *cnt = MARLNAV_CNT_EARLY ? cnt_e : kl->a.b.counters;
-                    const int64_t slots = MARLNAV_CNT_EARLY ? slots_e : kl->a.waves;
+                    uint64_t *cnt = kl->a.b.counters;
+                    const int64_t slots = kl->a.waves;
                     if (cnt) {
                         const int64_t sl = blk < slots ? blk : blk % slots;
                         if (c_trunc) atomicAdd((unsigned long long *)&cnt[0 * slots + sl], (unsigned long long)c_trunc);
@@ -762,11 +587,7 @@ __global__ void __launch_bounds__(64 * (A * (1 + PS) + HELP) * T)
             // writes the states, obstacles, target and rows of finished envs.
             bool fin = false;
             if (l < ne) {  // (the same env_end as wave 0's, on the same LDS inputs)
-                fin = env_end<A>(
-                          [&](int i) {
-                              return PS && fast ? row_half_flags(red[A * l + i].z, red[R + A * l + i].z)
-                                                : __float_as_uint(red[A * l + i].z);
-                          },
+                fin = env_end<A>([&](int i) { return __float_as_uint(red[A * l + i].z); },
                                  lds[BP::SN + l],
                                  reinterpret_cast<const uint8_t *>(lds + BP::TM)[l], pr.trunc_after)
                           .fin;

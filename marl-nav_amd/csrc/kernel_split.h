@@ -1382,23 +1382,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     if ((MARLNAV_AB & (1 << 19)) && tail_wg) return;
     if (!stored) store_tile();
     STAMP(6);
-#if MARLNAV_CLAIM_PROBE
-    // (A/B builds, timing only) the price of a
-    // cross-workgroup work list for the finished-env tail: every workgroup,
-    // after its stores, makes the one returning atomic a drain would need to
-    // claim from (or find empty) its XCD's shard of the list
-    if (wib == 0 && lane == 0) {
-        const unsigned x = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) & 7u;
-#if MARLNAV_STAMPS
-        const unsigned long long tc0 = wall_clock64();
-#endif
-        const unsigned v = atomicAdd(&g_claim_probe[x * 32], 1u);
-        if (v == 0xFFFFFFFFu) g_claim_probe[x * 32 + 1] = v;  // (the value is used: the wave waits for it)
-#if MARLNAV_STAMPS
-        *STAMP_PTR((size_t)gw * 24 + 23) = wall_clock64() - tc0;
-#endif
-    }
-#endif
     if (!OBS_ONLY && lane == 0 && (c_trunc | c_col | c_tar)) {
         KArgsK *kl = kargs_late<kHotKargsOff>();
         uint64_t *cnt = kl->a.b.counters;

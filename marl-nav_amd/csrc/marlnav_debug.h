@@ -149,7 +149,15 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // Round 6 (HISTORY.md; code in git history at 9a7feb1): MARLNAV_ONE_STAGE
 // (each wave gathers its agent's rows by per-lane dword LDS-DMA and moves it
 // before ONE barrier: bit-exact, slower at every shape, 65536x3x3 6.55 ->
-// 6.89 us, 16384x3x3 4.65 -> 4.73, 2^20 envs 68.7 -> 74.4).
+// 6.89 us, 16384x3x3 4.65 -> 4.73, 2^20 envs 68.7 -> 74.4). Round 6, code in
+// git history at a9bbeb6 (profiles/r06_ab_*.txt, r06_claim_probe.txt):
+// MARLNAV_STAGGER (late blocks per CU: never faster), MARLNAV_PAIR_SPLIT (two
+// waves per agent, the row's pairs split: bit-exact, 16384x3x3 4.65 ->
+// 4.67-4.75 us), MARLNAV_STAGE_AUX (staging cache policy: +-0 or slower),
+// MARLNAV_ACT_FIRST (action loads before the spans: +0.1 us),
+// MARLNAV_CNT_EARLY (+-0), MARLNAV_BLOCK_TILES (T blocks per workgroup:
+// bit-exact, 65536x3x3 6.48 -> 7.38 / 7.67 us), MARLNAV_CLAIM_PROBE (split
+// kernel: the claim of a cross-workgroup work list, +0.35 us at 4096x16x32).
 // Round 5 (DESIGN.md §5 "Round 5"; code in git history at deae14b):
 // MARLNAV_BLOCK_ENV_ROT / MARLNAV_SPLIT_ENV_ROT (the per-env phase on wave
 // block % A / workgroup % 4: no gain, and the general re-init thread index
@@ -177,56 +185,4 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // (profiles/r06_ab_packed_split.txt): off (A/B builds: 1)
 #ifndef MARLNAV_PACKED_SPLIT
 #define MARLNAV_PACKED_SPLIT 0
-#endif
-// Env-block kernel, pair-split instantiation (block_kernel PS: two waves
-// per agent, the row's target/obstacle pairs and its other-agent pairs on
-// different waves): 1 for the draw-wave grids (at most one block per CU),
-// 2 for every grid (A/B builds), 0 off
-#ifndef MARLNAV_PAIR_SPLIT
-#define MARLNAV_PAIR_SPLIT 0
-#endif
-// Env-block kernel: cache-policy bits of the staging LDS-DMA loads (actions
-// and spans; 0: default; A/B builds: 1 sc0, 2 nt, 16 sc1)
-#ifndef MARLNAV_STAGE_AUX
-#define MARLNAV_STAGE_AUX 0
-#endif
-// Split kernel (A/B builds, timing only): every workgroup makes one
-// returning atomic on a per-XCD counter after its stores - the claim a
-// cross-workgroup finished-env work list would cost (kernel_split.h)
-#ifndef MARLNAV_CLAIM_PROBE
-#define MARLNAV_CLAIM_PROBE 0
-#endif
-#if MARLNAV_CLAIM_PROBE
-__device__ unsigned g_claim_probe[8 * 32];
-#endif
-// Env-block kernel (A/B builds): a block barrier between the waves' action
-// loads and the spans' LDS-DMA (kernel_block.h)
-#ifndef MARLNAV_ACT_FIRST
-#define MARLNAV_ACT_FIRST 0
-#endif
-#ifndef MARLNAV_CNT_EARLY
-#define MARLNAV_CNT_EARLY 0
-#endif
-// Env-block kernel (A/B builds): env blocks per workgroup of the step kernel
-// at grids above the draw-wave size (1: one, the product)
-#ifndef MARLNAV_BLOCK_TILES
-#define MARLNAV_BLOCK_TILES 1
-#endif
-// Env-block kernel stagger (A/B builds, timing only; 0 in the product): the
-// blocks with (blockIdx / DIV) % MOD >= MOD - N sleep MARLNAV_STAGGER x 64
-// cycles before issuing any load, so the other blocks of their CU stage,
-// compute and store ahead of them (burst overlap between co-resident blocks;
-// VERDICT r5 item 3). At 1024 blocks dealt round-robin over 8 XCDs of 32 CUs,
-// blockIdx >> 8 is the block's slot on its CU.
-#ifndef MARLNAV_STAGGER
-#define MARLNAV_STAGGER 0
-#endif
-#ifndef MARLNAV_STAGGER_DIV
-#define MARLNAV_STAGGER_DIV 256
-#endif
-#ifndef MARLNAV_STAGGER_MOD
-#define MARLNAV_STAGGER_MOD 4
-#endif
-#ifndef MARLNAV_STAGGER_N
-#define MARLNAV_STAGGER_N 1
 #endif

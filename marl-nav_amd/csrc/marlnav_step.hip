@@ -371,10 +371,6 @@ struct BlockVariant {
     size_t lds;
     BlockFn step_draw;  // (or null) the step with a draw wave: grids of at most one block per CU
     int E;              // envs per block
-    BlockFn step_ps;    // (or null) the pair-split step (block_kernel PS) for the draw-wave grids
-    BlockFn step_ps_big;  // (or null; MARLNAV_PAIR_SPLIT 2, A/B builds) the same for larger grids
-    size_t lds_ps;      // its LDS
-    BlockFn step_tiles;   // (or null; MARLNAV_BLOCK_TILES > 1, A/B builds) T env blocks per workgroup
 };
 
 // compute units of the current device (the draw-wave rule: at most one
@@ -404,34 +400,10 @@ constexpr BlockFn block_draw_fn()
     else return nullptr;
 }
 
-// The pair-split instantiations (block_kernel PS): shapes whose half rows
-// are 16-byte pieces of the LDS row (A3/O3, A3/O1), with the draw wave
-// (HELP) for grids of at most one block per CU, and without it (larger
-// grids, MARLNAV_PAIR_SPLIT 2 only)
-template <int A, int O, bool HELP>
-constexpr BlockFn block_ps_fn()
-{
-    constexpr int D = BlockPlan<A, O>::D;
-    if constexpr (D % 4 == 0 && (2 + 2 * O) % 4 == 0 && (!HELP || O <= 3) &&
-                  (HELP ? MARLNAV_PAIR_SPLIT >= 1 : MARLNAV_PAIR_SPLIT >= 2))
-        return block_kernel<A, O, false, false, HELP, true>;
-    else return nullptr;
-}
-
-template <int A, int O>
-constexpr BlockFn block_tiles_fn()
-{
-    if constexpr (MARLNAV_BLOCK_TILES > 1)
-        return block_kernel<A, O, false, false, false, false, MARLNAV_BLOCK_TILES>;
-    else return nullptr;
-}
-
 #define MARLNAV_BLOCK_VARIANT(A, O)                                                    \
     {A, O, block_kernel<A, O, false, false>, block_kernel<A, O, true, false>,          \
      block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4,             \
-     block_draw_fn<A, O>(), BlockPlan<A, O>::E, block_ps_fn<A, O, true>(),            \
-     block_ps_fn<A, O, false>(), (size_t)BlockPlan<A, O, 2>::FLOATS * 4,              \
-     block_tiles_fn<A, O>()}
+     block_draw_fn<A, O>(), BlockPlan<A, O>::E}
 const BlockVariant kBlockVariants[] = {
     MARLNAV_BLOCK_VARIANT(3, 3),
     MARLNAV_BLOCK_VARIANT(3, 8),
@@ -457,7 +429,7 @@ const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers 
 }
 
 int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const MarlnavParams &pr,
-                 void *stream, const char *what, int waves = 0, size_t lds = 0, int tiles = 1)
+                 void *stream, const char *what, int waves = 0)
 {
     KArgs ka;
     ka.a = args;
@@ -472,10 +444,8 @@ int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const 
     int64_t h_P = args.P;
     void *kargs[] = {&h_states, &h_actions, &h_obstacles, &h_target, &h_step_num, &h_terminates,
                      &h_P, &ka};
-    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn),
-                                   dim3((unsigned)((ka.a.ntiles + tiles - 1) / tiles)),
-                                   dim3(64 * (waves ? waves : v.A) * tiles), kargs,
-                                   (lds ? lds : v.lds) * tiles, (hipStream_t)stream);
+    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)ka.a.ntiles),
+                                   dim3(64 * (waves ? waves : v.A)), kargs, v.lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
     return 0;
@@ -664,19 +634,8 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
             g_last_family = MARLNAV_FAMILY_BLOCK;
             // one block per CU (MI355X: 256 CUs) leaves a SIMD of each CU idle
             const int64_t nblk = (d->num_parallel + v->E - 1) / v->E;
-            if (!noisy && v->step_ps && nblk <= device_cus() && !b->fresh_states)
-                return launch_block(*v, v->step_ps, args, *pr, stream, "marlnav_step", 2 * v->A + 1,
-                                    v->lds_ps);
-            if (!noisy && v->step_ps_big && !b->fresh_states)
-                return launch_block(*v, v->step_ps_big, args, *pr, stream, "marlnav_step", 2 * v->A,
-                                    v->lds_ps);
             if (!noisy && v->step_draw && nblk <= device_cus() && !b->fresh_states)
                 return launch_block(*v, v->step_draw, args, *pr, stream, "marlnav_step", v->A + 1);
-            // (T blocks per workgroup meet the same barriers: only the native
-            // re-init without the fused normaliser has a block-uniform count)
-            if (!noisy && v->step_tiles && !b->fresh_states && !(pr->flags & MARLNAV_WRITE_OBS_NORM))
-                return launch_block(*v, v->step_tiles, args, *pr, stream, "marlnav_step", 0, 0,
-                                    MARLNAV_BLOCK_TILES);
             return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }
     const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);

@@ -2,6 +2,8 @@
 cross-workgroup finished-env work list would cost each split-kernel workgroup
 after its stores (MARLNAV_CLAIM_PROBE stamps build, slot 23 of wave 0 of each
 workgroup), and when those workgroups end relative to the kernel's last wave.
+The probe's code is in git history at a9bbeb6 (removed from the sources):
+  scripts/build_variant.sh stclaim a9bbeb6 -DMARLNAV_CLAIM_PROBE=1 -DMARLNAV_STAMPS=1
 usage: STAMPS_LIB=stclaim.so python scripts/diag/claim_rtt.py 4096x16x32"""
 import ctypes
 import os
