@@ -81,9 +81,6 @@ namespace {
 #include "kernel_reinit.h"
 #include "kernel_split.h"
 #include "kernel_block.h"
-#if MARLNAV_LANE_PROTO
-#include "kernel_lane.h"
-#endif
 
 // ----------------------------------------------------- native reinit kernel
 __global__ void reinit_all_kernel(int64_t P, int A, int S, int64_t env_offset, uint64_t sidx,
@@ -632,35 +629,6 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
             return launch_split(*v, noisy ? v->noisy : (own ? v->step_own : v->step), args, *pr,
                                 stream, "marlnav_step");
         }
-#if MARLNAV_LANE_PROTO
-    // (A/B prototype, kernel_lane.h: the env-lane kernel at A3/O3 grids of
-    // whole waves above one block per CU, native re-init, no normaliser/scaler)
-    if (family_allowed(MARLNAV_FAMILY_BLOCK) && d->num_agents == 3 && d->num_obstacles == 3 &&
-        d->obstacle_stride == 3 && !noisy && !b->fresh_states && d->num_parallel % 64 == 0 &&
-        d->num_parallel / 64 > device_cus() &&
-        !(pr->flags & (MARLNAV_WRITE_OBS_NORM | MARLNAV_SCALE_ACTIONS)) &&
-        select_block(d, args.b, false)) {
-        g_last_family = MARLNAV_FAMILY_BLOCK;
-        KArgs ka;
-        ka.a = args;
-        ka.p = *pr;
-        ka.a.W = 64;
-        ka.a.ntiles = d->num_parallel / 64;
-        float *h_states = args.b.states;
-        const float *h_actions = args.b.actions, *h_obstacles = args.b.obstacles,
-                    *h_target = args.b.target, *h_step_num = args.b.step_num;
-        const uint8_t *h_terminates = args.b.terminates;
-        int64_t h_P = args.P;
-        void *kargs[] = {&h_states, &h_actions, &h_obstacles, &h_target, &h_step_num, &h_terminates,
-                         &h_P, &ka};
-        hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(lane_kernel<3, 3>),
-                                       dim3((unsigned)((ka.a.ntiles + 3) / 4)), dim3(256), kargs,
-                                       (size_t)LanePlan<3, 3>::FLOATS * 4 * 4, (hipStream_t)stream);
-        if (e == hipSuccess) e = hipGetLastError();
-        if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "marlnav_step: %s", hipGetErrorString(e));
-        return 0;
-    }
-#endif
     if (family_allowed(MARLNAV_FAMILY_BLOCK))
         if (const BlockVariant *v = select_block(d, args.b, false)) {
             g_last_family = MARLNAV_FAMILY_BLOCK;
