@@ -169,6 +169,11 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // and re-observed by its own wave before the per-env barrier: bit-exact, but
 // 4096x16x32 11.66 -> 14.51 us, the lone wave's pair chains run one after the
 // other), MARLNAV_SPLIT_ENV_WT.
+// Env-block kernel, draw-wave instantiation: every lane moves all A agents of
+// its env, no move barrier (kernel_block.h RM; 0: off)
+#ifndef MARLNAV_RMOVE
+#define MARLNAV_RMOVE 0
+#endif
 // Env-block kernel: blocks with no finished env stream their rows from waves
 // 1..A-1 under the per-env phase (1), after it (0), or by shape (-1: the
 // product's choice, kBlockEarlyOut in kernel_block.h)
