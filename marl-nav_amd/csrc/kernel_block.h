@@ -17,7 +17,7 @@
 // packed observation rows are assembled in LDS and streamed out as one
 // contiguous span (a store instruction covers 1 KiB, 8 cache lines, where
 // register-row stores at a 48-byte lane stride touch 24).
-template <int A, int O, int SO = 0>
+template <int A, int O>
 struct BlockPlan {
     static constexpr int E = 64, R = E * A, D = 2 + 2 * O + 2 * (A - 1);
     static constexpr int NT = 64 * A;                      // threads per block
@@ -33,8 +33,7 @@ struct BlockPlan {
     static constexpr int LIST = (OBS + R * D + 3) & ~3;    // (E,) finished envs
     static constexpr int FLG = LIST + E;                   // [0] nfin, [1 + w] wave w coords bad
     static constexpr int FRESH = (FLG + 1 + A + 3) & ~3;   // (2O, E) fresh obstacle draws
-    static constexpr int STO = (FRESH + 2 * O * E + 3) & ~3;  // SO: (R, 5) moved states
-    static constexpr int FLOATS = STO + SO * R * 5;
+    static constexpr int FLOATS = FRESH + 2 * O * E;
     static_assert(A >= 2 && A <= 16, "one wave per agent");
 };
 
@@ -191,20 +190,13 @@ constexpr bool kBlockEarlyOut = MARLNAV_EARLY_OUT < 0 ? O >= 8 : MARLNAV_EARLY_O
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
 // re-init; none in most blocks) | rows and states stream out of LDS.
-// RM (MARLNAV_RMOVE, with HELP): in a full block every lane moves all A
-// agents of its env (the env's A action pairs in registers, A sin/cos
-// chains), keeps the moved rows in registers for its observation and writes
-// its own agent's moved row to a separate LDS region, so no block barrier
-// separates the move from the observation; the pair math is chosen per wave
-// from the lanes' own envs (both choices give the same bits).
-template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false, bool RM = false>
+template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false>
 __global__ void __launch_bounds__(64 * (A + HELP))
     block_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
                  const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
                  int64_t h_P, KArgs k)
 {
-    using BP = BlockPlan<A, O, RM ? 1 : 0>;
-    static_assert(!RM || (HELP && !OBS_ONLY && !NOISY), "redundant moves: the draw-wave step");
+    using BP = BlockPlan<A, O>;
     // NT: the agent waves' threads, over which every work loop is spread
     // (HELP: one more wave, w == A, draws the fresh obstacles and otherwise
     // only meets the barriers)
@@ -239,7 +231,6 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     const int64_t e0 = blk * E;
     const int ne = (int)((P - e0) < E ? (P - e0) : E);
     const bool full = ne == E;
-    const bool rm = RM && full;  // (block-uniform)
 
     // ---- this wave's actions (lane l: agent w of env l) into its own LDS
     // slots by LDS-DMA issued before the block's spans: the wave waits for
@@ -247,12 +238,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // evaluates the heading's sin/cos while the spans are still in flight,
     // not after the stage barrier
     float *actw = lds + BP::ACTW + 2 * E * (hw ? 0 : w);  // x at [l], y at [E + l]
-    float2 acts[A];
-    if (rm && !hw) {
-        const float2 *pa = reinterpret_cast<const float2 *>(h_actions) + (e0 + lane) * A;
-#pragma unroll
-        for (int i = 0; i < A; ++i) acts[i] = pa[i];
-    } else if (!OBS_ONLY && full && !hw) {
+    if (!OBS_ONLY && full && !hw) {
         const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
         __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
         __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
@@ -343,27 +329,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // the heading's sin/cos (environment.py:113-115, 131-137), under the
     // remaining staging latency
     float sn = 0.0f, c = 1.0f, a1 = 0.0f;
-    float snv[A], cv[A], a1v[A];
-    if (rm && !hw) {
-        int n = 0;
-#pragma unroll
-        for (int ww = 0; ww < A; ++ww)
-            if (w == ww) n = b.formation ? BS::after_actions(ww, true) : BS::after_actions(ww, false);
-        wait_vmcnt(n);
-        STAMPS_S(0);
-#pragma unroll
-        for (int i = 0; i < A; ++i) {
-            float a0 = acts[i].x;
-            a1v[i] = acts[i].y;
-            if (pr.flags & MARLNAV_SCALE_ACTIONS) {  // ActionScaler (utils.py:546-547)
-                KArgsK *kl = kargs_late<kHotKargsOff>();
-                a0 = kl->p.act_scale[0] * a0 + kl->p.act_mean[0];
-                a1v[i] = kl->p.act_scale[1] * a1v[i] + kl->p.act_mean[1];
-            }
-            sincos_k(clamp_t(a0, -kPiF, kPiF), &snv[i], &cv[i]);
-        }
-        STAMPS_S(1);
-    } else if (!OBS_ONLY && !hw) {
+    if (!OBS_ONLY && !hw) {
         if (full) {
             // span instructions this wave issued after its two action loads
             // (BlockSpans: the same table as the issue sites above)
@@ -406,7 +372,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // (below); read before the move writes LDS, so the reads overlap it
     // (a partial last block takes the IEEE path without checking)
     CoordRange crange;
-    if (full && !hw && !rm) {
+    if (full && !hw) {
         constexpr int NC = E * O * 2 + E * 2;  // OB and TG are adjacent spans
         static_assert(BP::TG == BP::OB + E * O * 2, "adjacent obstacle/target spans");
 #pragma unroll
@@ -418,57 +384,14 @@ __global__ void __launch_bounds__(64 * (A + HELP))
 
     // ---- _move_agents (environment.py:113-123), own row in registers
     float ox, oy, dx, dy;
-    float mv[A * 5];  // (rm: every agent of the lane's env, moved)
-    float *sto = rm ? lds + BP::STO : st;  // the moved states the later phases read
-    bool wfast = false;  // (rm: this wave's choice of the pair math)
-    if constexpr (RM) {
-        if (rm && !hw) {
-            const float *se = st + 5 * A * l;
-#pragma unroll
-            for (int i = 0; i < A * 5; ++i) mv[i] = se[i];
-            CoordRange cr;
-#pragma unroll
-            for (int i = 0; i < 2 * O; ++i) cr.add(lds[BP::OB + 2 * O * l + i]);
-            cr.add(lds[BP::TG + 2 * l]);
-            cr.add(lds[BP::TG + 2 * l + 1]);
-#pragma unroll
-            for (int i = 0; i < A; ++i) {
-                const float ddx = mv[5 * i + 2], ddy = mv[5 * i + 3];
-                const float ndx = cv[i] * ddx + (-snv[i]) * ddy;
-                const float ndy = snv[i] * ddx + cv[i] * ddy;
-                const float v = clamp_t(mv[5 * i + 4] + clamp_t(a1v[i], pr.min_accel, pr.max_accel),
-                                        pr.min_speed, pr.max_speed);
-                mv[5 * i] = mv[5 * i] + ndx * v;
-                mv[5 * i + 1] = mv[5 * i + 1] + ndy * v;
-                mv[5 * i + 2] = ndx;
-                mv[5 * i + 3] = ndy;
-                mv[5 * i + 4] = v;
-                cr.add(mv[5 * i]);
-                cr.add(mv[5 * i + 1]);
-            }
-            float mo[5];
-#pragma unroll
-            for (int i = 0; i < A; ++i)
-                if (w == i)
-#pragma unroll
-                    for (int q = 0; q < 5; ++q) mo[q] = mv[5 * i + q];
-#pragma unroll
-            for (int q = 0; q < 5; ++q) sto[5 * r + q] = mo[q];
-            ox = mo[0];
-            oy = mo[1];
-            dx = mo[2];
-            dy = mo[3];
-            wfast = __ballot(!cr.ok()) == 0ull;
-        }
-    }
-    if (!rm) {
+    {
         const float *s = st + 5 * r;
         ox = s[0];
         oy = s[1];
         dx = s[2];
         dy = s[3];
     }
-    if (!OBS_ONLY && !rm) {
+    if (!OBS_ONLY) {
         const float ndx = c * dx + (-sn) * dy;
         const float ndy = sn * dx + c * dy;
         float *s = st + 5 * r;
@@ -490,7 +413,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // reciprocal division (equal to IEEE there) when every coordinate of the
     // block (obstacles and targets above, moved agents here) passes coord_ok,
     // IEEE otherwise
-    if (full && !hw && !rm) {
+    if (full && !hw) {
         crange.add(ox);
         crange.add(oy);
         // one word for the block, written only by waves that found one (all
@@ -498,15 +421,10 @@ __global__ void __launch_bounds__(64 * (A + HELP))
         const bool bad = __ballot(!crange.ok()) != 0ull;
         if (lane == 0 && bad) *bad_word = 1;
     }
-    if (!rm) __syncthreads();  // (rm: no other wave's moved row is read)
+    __syncthreads();
     STAMP(2);
     // the moved states are final except in finished envs (re-stored below)
-    const bool fast = rm ? wfast : full && *bad_word == 0;
-    if constexpr (RM) {  // (a partial block: its moved rows, for the register-row observation)
-        if (!rm && row_on)
-#pragma unroll
-            for (int i = 0; i < A * 5; ++i) mv[i] = st[5 * A * l + i];
-    }
+    const bool fast = full && *bad_word == 0;
 
     // ---- observations of the moved state + reward terms (:99-100)
     float4 *red = reinterpret_cast<float4 *>(lds + BP::RED);
@@ -517,15 +435,15 @@ __global__ void __launch_bounds__(64 * (A + HELP))
         bool unused = true;
         if (__builtin_expect(fast, 1) && !MARLNAV_AB_NOREFC && pr.bond_sharpness == 1.0f &&
             pr.max_at_prop_d == 2.0f)
-            ro = observe_row_own<A, O, !OBS_ONLY, true, true>(RM ? mv : st + 5 * A * l, lds + BP::OB + 2 * O * l,
+            ro = observe_row_own<A, O, !OBS_ONLY, true, true>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
                                                               lds + BP::TG + 2 * l, w, ox, oy, dx,
                                                               dy, rowv, pr, unused);
         else if (__builtin_expect(fast, 1))
-            ro = observe_row_own<A, O, !OBS_ONLY, true>(RM ? mv : st + 5 * A * l, lds + BP::OB + 2 * O * l,
+            ro = observe_row_own<A, O, !OBS_ONLY, true>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
                                                         lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
                                                         rowv, pr, unused);
         else
-            ro = observe_row_own<A, O, !OBS_ONLY, false>(RM ? mv : st + 5 * A * l, lds + BP::OB + 2 * O * l,
+            ro = observe_row_own<A, O, !OBS_ONLY, false>(st + 5 * A * l, lds + BP::OB + 2 * O * l,
                                                          lds + BP::TG + 2 * l, w, ox, oy, dx, dy,
                                                          rowv, pr, unused);
 #if MARLNAV_STAMPS && MARLNAV_SUBSTAMPS
@@ -556,7 +474,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     if (!OBS_ONLY) {
         int *list = reinterpret_cast<int *>(lds + BP::LIST);
         int *flg = reinterpret_cast<int *>(lds + BP::FLG);
-        const BlockEnvs<A, O, D> ev{sto, lds + BP::OB, lds + BP::TG, obs_rows, e0};
+        const BlockEnvs<A, O, D> ev{st, lds + BP::OB, lds + BP::TG, obs_rows, e0};
         // ---- per-env reductions, terminal logic (wave 0, one lane per env)
         if (w == 0) {
             if (MARLNAV_ENV_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_ENV_PRIO);  // (A/B builds)
@@ -678,7 +596,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
             early = kBlockEarlyOut<A, O> && full && !norm && fm == 0ull;
             if (early && !(MARLNAV_AB & 2))
                 block_store2<E * A * D, E * A * 5, NT - 64>(
-                    gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)), sto, tid - 64, wt);
+                    gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)), st, tid - 64, wt);
             STAMPX(0);
             if (fm && !(MARLNAV_AB & 1)) {
                 if (MARLNAV_REINIT_PRIO) __builtin_amdgcn_s_setprio(MARLNAV_REINIT_PRIO);  // (A/B builds)
@@ -722,14 +640,14 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     } else if (!OBS_ONLY && full && !norm) {  // ---- stream the block out
         if (!(MARLNAV_AB & 2) && !early)
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)),
-                                               sto, tid, wt);  // (E = 64: whole 16-byte pieces)
+                                               st, tid, wt);  // (E = 64: whole 16-byte pieces)
     } else if (!OBS_ONLY && full && NT % D == 0) {
         // ---- the same with the fused ObsNormalizer (utils.py:519-532):
         // thread tid only ever meets feature tid % D (NT is a multiple of D),
         // so its mean and scale are loaded once; every LDS read and every
         // division is issued ahead of the stores
         block_store2<E * A * D, E * A * 5, NT>(gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)),
-                                               sto, tid, wt);
+                                               st, tid, wt);
         KArgsK *kl = kargs_late<kHotKargsOff>();
         const int kk = tid % D;
         const float m = kl->a.b.norm_mean[kk], sc = kl->a.b.norm_scale[kk];
@@ -773,7 +691,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
                     gn[i] = v;
             }
         }
-        block_store(in_sgpr(bo.states_out + e0 * (A * 5)), sto, nrow * 5, tid, NT, wt);
+        block_store(in_sgpr(bo.states_out + e0 * (A * 5)), st, nrow * 5, tid, NT, wt);
     }
     STAMP(6);
 #if MARLNAV_STAMPS

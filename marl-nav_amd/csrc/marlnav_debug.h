@@ -160,7 +160,9 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // kernel: the claim of a cross-workgroup work list, +0.35 us at 4096x16x32);
 // at 7e0c2a8: MARLNAV_LANE_PROTO (kernel_lane.h, an env-lane kernel: one wave per
 // 64 whole envs, no block barrier; slower at every size, 65536x3x3 6.51 ->
-// 7.20 us without its re-init).
+// 7.20 us without its re-init); at c5c92fc: MARLNAV_RMOVE (draw-wave
+// instantiation: every lane moves all A agents of its env, no move barrier;
+// bit-exact, +0.4 us at 16384x3x3).
 // Round 5 (DESIGN.md §5 "Round 5"; code in git history at deae14b):
 // MARLNAV_BLOCK_ENV_ROT / MARLNAV_SPLIT_ENV_ROT (the per-env phase on wave
 // block % A / workgroup % 4: no gain, and the general re-init thread index
@@ -169,11 +171,6 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // and re-observed by its own wave before the per-env barrier: bit-exact, but
 // 4096x16x32 11.66 -> 14.51 us, the lone wave's pair chains run one after the
 // other), MARLNAV_SPLIT_ENV_WT.
-// Env-block kernel, draw-wave instantiation: every lane moves all A agents of
-// its env, no move barrier (kernel_block.h RM; 0: off)
-#ifndef MARLNAV_RMOVE
-#define MARLNAV_RMOVE 0
-#endif
 // Env-block kernel: blocks with no finished env stream their rows from waves
 // 1..A-1 under the per-env phase (1), after it (0), or by shape (-1: the
 // product's choice, kBlockEarlyOut in kernel_block.h)

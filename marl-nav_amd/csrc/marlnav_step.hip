@@ -371,7 +371,6 @@ struct BlockVariant {
     size_t lds;
     BlockFn step_draw;  // (or null) the step with a draw wave: grids of at most one block per CU
     int E;              // envs per block
-    size_t lds_draw;    // its LDS (MARLNAV_RMOVE: with the moved-state region)
 };
 
 // compute units of the current device (the draw-wave rule: at most one
@@ -397,16 +396,14 @@ int device_cus()
 template <int A, int O>
 constexpr BlockFn block_draw_fn()
 {
-    if constexpr (O <= 3 && MARLNAV_DRAW_WAVE)
-        return block_kernel<A, O, false, false, true, MARLNAV_RMOVE != 0>;
+    if constexpr (O <= 3 && MARLNAV_DRAW_WAVE) return block_kernel<A, O, false, false, true>;
     else return nullptr;
 }
 
 #define MARLNAV_BLOCK_VARIANT(A, O)                                                    \
     {A, O, block_kernel<A, O, false, false>, block_kernel<A, O, true, false>,          \
      block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4,             \
-     block_draw_fn<A, O>(), BlockPlan<A, O>::E,                                        \
-     (size_t)BlockPlan<A, O, MARLNAV_RMOVE != 0>::FLOATS * 4}
+     block_draw_fn<A, O>(), BlockPlan<A, O>::E}
 const BlockVariant kBlockVariants[] = {
     MARLNAV_BLOCK_VARIANT(3, 3),
     MARLNAV_BLOCK_VARIANT(3, 8),
@@ -432,7 +429,7 @@ const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers 
 }
 
 int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const MarlnavParams &pr,
-                 void *stream, const char *what, int waves = 0, size_t lds = 0)
+                 void *stream, const char *what, int waves = 0)
 {
     KArgs ka;
     ka.a = args;
@@ -448,8 +445,7 @@ int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const 
     void *kargs[] = {&h_states, &h_actions, &h_obstacles, &h_target, &h_step_num, &h_terminates,
                      &h_P, &ka};
     hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)ka.a.ntiles),
-                                   dim3(64 * (waves ? waves : v.A)), kargs, lds ? lds : v.lds,
-                                   (hipStream_t)stream);
+                                   dim3(64 * (waves ? waves : v.A)), kargs, v.lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
     return 0;
@@ -639,8 +635,7 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
             // one block per CU (MI355X: 256 CUs) leaves a SIMD of each CU idle
             const int64_t nblk = (d->num_parallel + v->E - 1) / v->E;
             if (!noisy && v->step_draw && nblk <= device_cus() && !b->fresh_states)
-                return launch_block(*v, v->step_draw, args, *pr, stream, "marlnav_step", v->A + 1,
-                                    v->lds_draw);
+                return launch_block(*v, v->step_draw, args, *pr, stream, "marlnav_step", v->A + 1);
             return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }
     const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
