@@ -188,6 +188,11 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // The same in the pair-split kernel's split_pairs (A16/O32, A3/O8 small
 // grids): 4096x16x32 11.19 -> 11.33 us, 1024x3x8 and 2048x16x32 unchanged
 // (profiles/r06_ab_packed_split.txt): off (A/B builds: 1)
+// Env-block kernel (A/B builds): tiles per workgroup, software-pipelined
+// (block_kernel TP; 1: one, the product)
+#ifndef MARLNAV_BLOCK_PIPE
+#define MARLNAV_BLOCK_PIPE 1
+#endif
 #ifndef MARLNAV_PACKED_SPLIT
 #define MARLNAV_PACKED_SPLIT 0
 #endif
