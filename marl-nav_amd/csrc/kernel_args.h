@@ -137,24 +137,6 @@ __device__ __forceinline__ void wait_vmcnt(int n)
     }
 }
 
-// the same for 0..15 (the pipelined env-block kernel's waits over two
-// tiles' staging loads)
-__device__ __forceinline__ void wait_vmcnt16(int n)
-{
-    if (n < 8) return wait_vmcnt(n);
-    switch (n) {
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-
 // plain copy of n elements (partial tiles)
 template <class T>
 __device__ __forceinline__ void copy_span(const T *__restrict__ src, T *__restrict__ dst, int n,

@@ -75,32 +75,6 @@ struct BlockSpans {
     }
 };
 
-// Issue a full block's staging loads (LDS-DMA): this wave's own actions
-// first (lane l: agent w of env l, into its LDS slots), then the block's
-// spans (span k by wave k % A). The draw wave (w == A) issues none.
-template <int A, int O, bool OBS_ONLY>
-__device__ __forceinline__ void block_stage_issue(const StepPtrs &b, const float *h_actions,
-                                                  int64_t e0, float *lds, int w, unsigned lane)
-{
-    using BP = BlockPlan<A, O>;
-    using BS = BlockSpans<A, O>;
-    constexpr int E = BP::E;
-    if (!OBS_ONLY && w < A) {
-        float *actw = lds + BP::ACTW + 2 * E * w;  // x at [l], y at [E + l]
-        const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
-        __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
-        __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
-    }
-    block_glds<BS::NB[0]>(BS::K[0], A, w, b.states + e0 * (A * 5), lds + BP::ST, lane);
-    block_glds<BS::NB[1]>(BS::K[1], A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
-    block_glds<BS::NB[2]>(BS::K[2], A, w, b.target + e0 * 2, lds + BP::TG, lane);
-    if (!OBS_ONLY) {
-        block_glds<BS::NB[3]>(BS::K[3], A, w, b.step_num + e0, lds + BP::SN, lane);
-        block_glds<BS::NB[4]>(BS::K[4], A, w, b.terminates + e0, lds + BP::TM, lane);
-        if (b.formation) block_glds<BS::NB[5]>(BS::K[5], A, w, b.formation, lds + BP::FORM, lane);
-    }
-}
-
 // plain strided copy of n elements by the block's NT threads (partial block)
 template <class T>
 __device__ __forceinline__ void block_copy(const T *__restrict__ src, T *__restrict__ dst, int n,
@@ -216,18 +190,11 @@ constexpr bool kBlockEarlyOut = MARLNAV_EARLY_OUT < 0 ? O >= 8 : MARLNAV_EARLY_O
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
 // waves 1..A-1 re-initialise and re-observe the finished envs (native
 // re-init; none in most blocks) | rows and states stream out of LDS.
-//
-// TP > 1 (A/B builds, MARLNAV_BLOCK_PIPE): TP consecutive env blocks per
-// workgroup of A waves, one after the other, software-pipelined: every
-// tile's staging loads are issued at entry, tile 0 waits for its own only,
-// and the later tiles' loads have landed before tile 0's first store (so a
-// later tile's waits never wait for the earlier tiles' stores, which drain
-// under its compute). Full blocks of the native step only (the host's rule).
-template <int N>
-struct TileIdx {
-    static constexpr int value = N;
-};
-template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false, int TP = 1>
+// (Two blocks per workgroup, software-pipelined - tile 1's loads under tile
+// 0's compute, tile 0's stores under tile 1's - measured bit-exact and
+// slower, 65536x3x3 6.44 -> 9.45 us: profiles/r06_ab_pipe.txt, code at
+// 16437ed.)
+template <int A, int O, bool OBS_ONLY, bool NOISY, bool HELP = false>
 __global__ void __launch_bounds__(64 * (A + HELP))
     block_kernel(float *h_states, const float *h_actions, const float *h_obstacles,
                  const float *h_target, const float *h_step_num, const uint8_t *h_terminates,
@@ -239,9 +206,8 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // only meets the barriers)
     constexpr int E = BP::E, R = BP::R, D = BP::D, NT = BP::NT;
     static_assert(!HELP || (!OBS_ONLY && !NOISY), "the draw wave serves the native re-init step");
-    static_assert(TP == 1 || (TP == 2 && !HELP && !OBS_ONLY), "pipelined tiles: two full blocks of the step");
     (void)k;  // read through kargs_late<kHotKargsOff>()
-    extern __shared__ __attribute__((aligned(16))) float lds_wg[];
+    extern __shared__ __attribute__((aligned(16))) float lds[];
 #if MARLNAV_STAMPS
     unsigned long long t_entry;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry));
@@ -263,28 +229,12 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     b.step_num = const_cast<float *>(h_step_num);
     b.terminates = const_cast<uint8_t *>(h_terminates);
     using BS = BlockSpans<A, O>;
-    // (TP > 1: every tile's staging loads, in tile order)
-    if constexpr (TP > 1) {
-#pragma unroll
-        for (int s = 0; s < TP; ++s)
-            block_stage_issue<A, O, OBS_ONLY>(b, h_actions, ((int64_t)blockIdx.x * TP + s) * BP::E,
-                                              lds_wg + s * BP::FLOATS, w, lane);
-    }
-    // (TP > 1: span instructions this wave issues per tile after its two
-    // action loads; BlockSpans: the same table as the issue sites)
-    int nspan_tp = 0;
-    if constexpr (TP > 1) {
-#pragma unroll
-        for (int ww = 0; ww < A; ++ww)
-            if (w == ww) nspan_tp = b.formation ? BS::after_actions(ww, true) : BS::after_actions(ww, false);
-    }
-    // one env block (TP > 1: tile S of the workgroup's TP; a lambda, not a
-    // loop: a loop around the body changed the product instantiation's
-    // register allocation, 88 -> 114 VGPRs)
-    auto tile = [&](auto s_c) __attribute__((always_inline)) {
-    constexpr int s = decltype(s_c)::value;
-    float *lds = lds_wg + s * BP::FLOATS;
-    const int64_t blk = (int64_t)blockIdx.x * TP + s;
+    // The block's phases are the body of a lambda called once: this form
+    // gives block_kernel<3,3> 87 VGPRs and no SGPR spill lanes where the
+    // plain body had 88 and 4 (65536x3x3 6.53 -> 6.44 us steady, 32768x3x3
+    // 5.30 -> 5.23, same box: profiles/r06_ab_pipe.txt)
+    auto block = [&]() __attribute__((always_inline)) {
+    const int64_t blk = blockIdx.x;
     const int64_t gw = blk * (A + HELP) + w;  // stamps slot
     STAMP(0);
     float *st = lds + BP::ST;
@@ -298,27 +248,24 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     // evaluates the heading's sin/cos while the spans are still in flight,
     // not after the stage barrier
     float *actw = lds + BP::ACTW + 2 * E * (hw ? 0 : w);  // x at [l], y at [E + l]
-    if (TP == 1 && !OBS_ONLY && full && !hw) {
+    if (!OBS_ONLY && full && !hw) {
         const float *pa = h_actions + ((e0 + lane) * A + w) * 2;
         __builtin_amdgcn_global_load_lds(pa, (LdsVoid *)actw, 4, 0, 0);
         __builtin_amdgcn_global_load_lds(pa + 1, (LdsVoid *)(actw + E), 4, 0, 0);
     }
-    // ---- stage the block (spans spread over the waves: span k by wave k % A;
-    // TP > 1: issued at entry)
+    // ---- stage the block (spans spread over the waves: span k by wave k % A)
     static_assert(BS::NB[0] == R * 20 && BS::NB[1] == E * O * 8 && BS::NB[2] == E * 8 &&
                       BS::NB[3] == E * 4 && BS::NB[4] == E && BS::NB[5] == (5 * A + 2) * 4,
                   "span table and LDS plan agree");
     if (full) {
-        if constexpr (TP == 1) {
-            block_glds<BS::NB[0]>(BS::K[0], A, w, b.states + e0 * (A * 5), st, lane);
-            block_glds<BS::NB[1]>(BS::K[1], A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
-            block_glds<BS::NB[2]>(BS::K[2], A, w, b.target + e0 * 2, lds + BP::TG, lane);
-            if (!OBS_ONLY) {
-                block_glds<BS::NB[3]>(BS::K[3], A, w, b.step_num + e0, lds + BP::SN, lane);
-                block_glds<BS::NB[4]>(BS::K[4], A, w, b.terminates + e0, lds + BP::TM, lane);
-                if (b.formation)
-                    block_glds<BS::NB[5]>(BS::K[5], A, w, b.formation, lds + BP::FORM, lane);
-            }
+        block_glds<BS::NB[0]>(BS::K[0], A, w, b.states + e0 * (A * 5), st, lane);
+        block_glds<BS::NB[1]>(BS::K[1], A, w, b.obstacles + e0 * (O * 2), lds + BP::OB, lane);
+        block_glds<BS::NB[2]>(BS::K[2], A, w, b.target + e0 * 2, lds + BP::TG, lane);
+        if (!OBS_ONLY) {
+            block_glds<BS::NB[3]>(BS::K[3], A, w, b.step_num + e0, lds + BP::SN, lane);
+            block_glds<BS::NB[4]>(BS::K[4], A, w, b.terminates + e0, lds + BP::TM, lane);
+            if (b.formation)
+                block_glds<BS::NB[5]>(BS::K[5], A, w, b.formation, lds + BP::FORM, lane);
         }
     } else if (!hw) {
         const int nr = ne * A;
@@ -393,17 +340,13 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     float sn = 0.0f, c = 1.0f, a1 = 0.0f;
     if (!OBS_ONLY && !hw) {
         if (full) {
-            if constexpr (TP == 1) {
-                // span instructions this wave issued after its two action loads
-                // (BlockSpans: the same table as the issue sites above)
-                int n = 0;
+            // span instructions this wave issued after its two action loads
+            // (BlockSpans: the same table as the issue sites above)
+            int n = 0;
 #pragma unroll
-                for (int ww = 0; ww < A; ++ww)
-                    if (w == ww) n = b.formation ? BS::after_actions(ww, true) : BS::after_actions(ww, false);
-                wait_vmcnt(n);
-            } else if constexpr (s == 0) {  // (and the later tiles' loads)
-                wait_vmcnt16(nspan_tp + (TP - 1) * (2 + nspan_tp));
-            }
+            for (int ww = 0; ww < A; ++ww)
+                if (w == ww) n = b.formation ? BS::after_actions(ww, true) : BS::after_actions(ww, false);
+            wait_vmcnt(n);
         }
         float a0 = actw[lane];
         a1 = actw[E + lane];
@@ -425,8 +368,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     const int nrow = ne * A;
     int *bad_word = reinterpret_cast<int *>(lds + BP::FLG) + 1;  // any coordinate off the fast range
     if (tid == 0) *bad_word = 0;
-    if constexpr (TP == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
-    else if constexpr (s == 0) wait_vmcnt16((TP - 1) * (2 + nspan_tp));  // (later tiles: landed before tile 0 stores)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
     STAMPS_S(2);  // (substamps: every span this wave issued landed)
     __syncthreads();
     STAMP(1);
@@ -523,9 +465,6 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     __syncthreads();
     STAMP(3);
     if (MARLNAV_AB & 16384) return;  // (AB 16384: timing only - observed, then exit)
-    // (TP > 1: the later tiles' staging loads land before this tile's first
-    // store, so no later wait counts a store)
-    if constexpr (TP > 1 && s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the output pointers, read again from the kernarg segment here: no
     // scalar register holds them through the observation, where the entry
     // copies spilled 14 SGPRs to VGPR lanes (65536x3x3 6.55 -> 6.33 us,
@@ -775,7 +714,6 @@ __global__ void __launch_bounds__(64 * (A + HELP))
     }
 #endif
     (void)gw;
-    };  // tile
-    tile(TileIdx<0>{});
-    if constexpr (TP > 1) tile(TileIdx<1>{});
+    };  // block
+    block();
 }

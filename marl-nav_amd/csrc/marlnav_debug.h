@@ -162,7 +162,9 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // 64 whole envs, no block barrier; slower at every size, 65536x3x3 6.51 ->
 // 7.20 us without its re-init); at c5c92fc: MARLNAV_RMOVE (draw-wave
 // instantiation: every lane moves all A agents of its env, no move barrier;
-// bit-exact, +0.4 us at 16384x3x3).
+// bit-exact, +0.4 us at 16384x3x3); at 16437ed: MARLNAV_BLOCK_PIPE (two
+// env blocks per workgroup, software-pipelined: bit-exact, 65536x3x3 6.44 ->
+// 9.45 us, profiles/r06_ab_pipe.txt).
 // Round 5 (DESIGN.md §5 "Round 5"; code in git history at deae14b):
 // MARLNAV_BLOCK_ENV_ROT / MARLNAV_SPLIT_ENV_ROT (the per-env phase on wave
 // block % A / workgroup % 4: no gain, and the general re-init thread index
@@ -188,11 +190,6 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // The same in the pair-split kernel's split_pairs (A16/O32, A3/O8 small
 // grids): 4096x16x32 11.19 -> 11.33 us, 1024x3x8 and 2048x16x32 unchanged
 // (profiles/r06_ab_packed_split.txt): off (A/B builds: 1)
-// Env-block kernel (A/B builds): tiles per workgroup, software-pipelined
-// (block_kernel TP; 1: one, the product)
-#ifndef MARLNAV_BLOCK_PIPE
-#define MARLNAV_BLOCK_PIPE 1
-#endif
 #ifndef MARLNAV_PACKED_SPLIT
 #define MARLNAV_PACKED_SPLIT 0
 #endif

@@ -371,7 +371,6 @@ struct BlockVariant {
     size_t lds;
     BlockFn step_draw;  // (or null) the step with a draw wave: grids of at most one block per CU
     int E;              // envs per block
-    BlockFn step_pipe;  // (or null; MARLNAV_BLOCK_PIPE > 1, A/B builds) pipelined tiles per workgroup
 };
 
 // compute units of the current device (the draw-wave rule: at most one
@@ -401,19 +400,10 @@ constexpr BlockFn block_draw_fn()
     else return nullptr;
 }
 
-// The pipelined instantiation (block_kernel TP = MARLNAV_BLOCK_PIPE; A/B builds)
-template <int A, int O>
-constexpr BlockFn block_pipe_fn()
-{
-    if constexpr (MARLNAV_BLOCK_PIPE > 1)
-        return block_kernel<A, O, false, false, false, MARLNAV_BLOCK_PIPE>;
-    else return nullptr;
-}
-
 #define MARLNAV_BLOCK_VARIANT(A, O)                                                    \
     {A, O, block_kernel<A, O, false, false>, block_kernel<A, O, true, false>,          \
      block_kernel<A, O, false, true>, (size_t)BlockPlan<A, O>::FLOATS * 4,             \
-     block_draw_fn<A, O>(), BlockPlan<A, O>::E, block_pipe_fn<A, O>()}
+     block_draw_fn<A, O>(), BlockPlan<A, O>::E}
 const BlockVariant kBlockVariants[] = {
     MARLNAV_BLOCK_VARIANT(3, 3),
     MARLNAV_BLOCK_VARIANT(3, 8),
@@ -439,7 +429,7 @@ const BlockVariant *select_block(const MarlnavDims *d, const MarlnavStepBuffers 
 }
 
 int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const MarlnavParams &pr,
-                 void *stream, const char *what, int waves = 0, int tiles = 1)
+                 void *stream, const char *what, int waves = 0)
 {
     KArgs ka;
     ka.a = args;
@@ -454,10 +444,8 @@ int launch_block(const BlockVariant &v, BlockFn fn, const StepArgs &args, const 
     int64_t h_P = args.P;
     void *kargs[] = {&h_states, &h_actions, &h_obstacles, &h_target, &h_step_num, &h_terminates,
                      &h_P, &ka};
-    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn),
-                                   dim3((unsigned)(ka.a.ntiles / tiles)),
-                                   dim3(64 * (waves ? waves : v.A)), kargs, v.lds * tiles,
-                                   (hipStream_t)stream);
+    hipError_t e = hipLaunchKernel(reinterpret_cast<const void *>(fn), dim3((unsigned)ka.a.ntiles),
+                                   dim3(64 * (waves ? waves : v.A)), kargs, v.lds, (hipStream_t)stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail(MARLNAV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
     return 0;
@@ -648,11 +636,6 @@ int marlnav_step(const MarlnavDims *d, const MarlnavParams *pr_in, const Marlnav
             const int64_t nblk = (d->num_parallel + v->E - 1) / v->E;
             if (!noisy && v->step_draw && nblk <= device_cus() && !b->fresh_states)
                 return launch_block(*v, v->step_draw, args, *pr, stream, "marlnav_step", v->A + 1);
-            // (A/B builds: pipelined tiles, whole workgroups of full blocks only)
-            if (!noisy && v->step_pipe && nblk > device_cus() &&
-                d->num_parallel % ((int64_t)v->E * MARLNAV_BLOCK_PIPE) == 0)
-                return launch_block(*v, v->step_pipe, args, *pr, stream, "marlnav_step", 0,
-                                    MARLNAV_BLOCK_PIPE);
             return launch_block(*v, noisy ? v->noisy : v->step, args, *pr, stream, "marlnav_step");
         }
     const KernelPair k = select_kernels(d->num_agents, d->num_obstacles);
