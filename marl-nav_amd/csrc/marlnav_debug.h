@@ -190,6 +190,13 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // The same in the pair-split kernel's split_pairs (A16/O32, A3/O8 small
 // grids): 4096x16x32 11.19 -> 11.33 us, 1024x3x8 and 2048x16x32 unchanged
 // (profiles/r06_ab_packed_split.txt): off (A/B builds: 1)
+// Split kernel, few-obstacle spread shapes (A3/O8): a finished env's fresh
+// rows from obstacle pairs computed speculatively at stage time, written by
+// its own wave (1), or the workgroup-wide fused re-init pass after a barrier
+// (0; A/B builds). kernel_split.h kSplitSpec.
+#ifndef MARLNAV_SPLIT_SPEC
+#define MARLNAV_SPLIT_SPEC 1
+#endif
 #ifndef MARLNAV_PACKED_SPLIT
 #define MARLNAV_PACKED_SPLIT 0
 #endif

@@ -240,6 +240,44 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
     assert (tot[1] > 0 or steps < 10) and (tot[0] > 0 or steps < ep)  # terminal paths hit
 
 
+@pytest.mark.parametrize("P,A,O,template", [(1000 + 3, 3, 8, False), (2048 + 5, 3, 8, False),
+                                            (1000 + 3, 3, 8, True)])
+def test_native_a3o8_finished_env_paths_bit_exact_vs_oracle(pkg, P, A, O, template):
+    """The split kernel's A3/O8 finished envs (native re-init, two-step
+    episodes: many finish every step) through both of its paths: with the
+    formation template (kSplitSpec: the fresh rows from obstacle pairs
+    computed at stage time, written by the env's own wave) and without it (a
+    C-ABI caller that passes no formation_obs: the workgroup-wide fused pass),
+    at LPR 8 (1003 envs, a partial last tile) and LPR 4 (2053 envs)."""
+    g = torch.Generator().manual_seed(P + 17 * template)
+    env = make_env(pkg, P, A, O, episode_len=2, seed=7)
+    if not template:
+        env._formation_obs = None
+        env._configure()
+    dm, pr = oracle_params(env)
+    form = np_(env._formation)
+    st, ob, tg = orc.reinit_all(dm, pr, form, 0)
+    sn = np.zeros(P, np.float32)
+    te = np.zeros(P, np.bool_)
+    n_fin = 0
+    for k in range(6):
+        acts = torch.stack([(torch.rand(P, A, generator=g) - 0.5) * 0.8,
+                            (torch.rand(P, A, generator=g) - 0.5) * 1.2], 2)
+        exp = orc.step(dm, pr, st, ob, tg, sn, te, acts.numpy(), formation=form, step_idx=k + 1)
+        obs, rew, term, trunc = env.step(acts.to(DEV))
+        where = f"P{P} template={template} step {k + 1}"
+        for got, key in ((env.states, "states"), (env.obstacles, "obstacles"),
+                         (env.target, "target"), (rew, "reward"), (term, "terminated"),
+                         (trunc, "truncated")):
+            np.testing.assert_array_equal(np_(got), exp[key], where + " " + key)
+        fg, fo = orc.split_obs(np_(obs._packed), A, O), orc.split_obs(exp["obs"], A, O)
+        assert_obs_close(fg, dict(zip(OBS_FIELDS, fo)), prefix="", exact=True, where=where)
+        st, ob, tg, sn, te = (exp[x] for x in ("states", "obstacles", "target", "step_num",
+                                               "terminates"))
+        n_fin += int((exp["step_num"] == 0.0).sum())
+    assert n_fin > 0  # the finished-env paths ran
+
+
 def test_threshold_proximity_native_65536(pkg):
     """on the headline workload (65 536 x 3 x 3, native
     re-init, random turns, 100 steps) count the observation entries within
