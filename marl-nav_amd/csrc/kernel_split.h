@@ -151,15 +151,6 @@ __host__ __device__ constexpr int split_tile_pad(int BOND, int F0, int K, int R)
     return best;
 }
 
-// kSplitSpec shapes (below): few-obstacle spread shapes whose fresh obstacle
-// pairs (every env, agent and obstacle of the workgroup) take one item per
-// lane of the three waves that wait out wave 0's per-env phase
-__host__ __device__ constexpr bool split_spec_shape(int A, int O, int LPR)
-{
-    return A * (1 + O + (A - 1)) >= 32 && O <= 8 && (A - 1) % LPR != 0 &&
-           kWavesPerBlock * (64 / LPR / A) * A * O <= 64 * (kWavesPerBlock - 1) && MARLNAV_SPLIT_SPEC;
-}
-
 template <int A, int O, int LPR>
 struct SplitPlan {
     static constexpr int EPW = 64 / LPR / A;  // envs per wave
@@ -197,15 +188,7 @@ struct SplitPlan {
     // (kSplitSpread shapes with O <= 8: the formation alone at FTP, for the
     // fused native re-init pass: MARLNAV_SPLIT_FORM_LDS)
     static constexpr int PRE = (FTP + (kSplitTpl<A, O> ? NCP : (kSplitSpread<A, O> && O <= 8 && MARLNAV_SPLIT_FORM_LDS ? NF : 0)) + 3) & ~3;
-    // (kSplitSpec shapes) the formation, its observation template (A x A
-    // float2: raw bearing, distance) and the speculative fresh obstacle pairs
-    // (EW x A x O float2: bearing, distance) that waves 1..3 park for the
-    // finished envs' waves
-    static constexpr bool SPEC = split_spec_shape(A, O, LPR);
-    static constexpr int SFORM = PRE + (kSplitSpread<A, O> && O <= 8 ? 2 * O * EW : 0);
-    static constexpr int STPL = SFORM + (SPEC ? (5 * A + 2 + 3) & ~3 : 0);
-    static constexpr int SPAIR = STPL + (SPEC ? 2 * A * A : 0);
-    static constexpr int BLK = SPAIR + (SPEC ? 2 * A * O * EW : 0);
+    static constexpr int BLK = PRE + (kSplitSpread<A, O> && O <= 8 ? 2 * O * EW : 0);
     static_assert(EPW >= 1, "an env's rows must fit one wave");
 };
 
@@ -274,24 +257,6 @@ struct SplitTerms {
 // angle/distance back from the LDS row.
 template <int A, int O, int LPR>
 constexpr bool kSplitTgtInAg = (A - 1) % LPR != 0;
-
-// The fresh env's obstacle pairs computed speculatively, for every env of
-// the workgroup (native re-init, formation template present), by waves 1..3
-// while wave 0 runs the per-env phase (they otherwise wait at its barrier):
-// one (env, agent, obstacle) item per lane - the Philox draw, the pair with
-// the formation agent - parked in LDS with the formation and its template.
-// A finished env's rows are then written by its own wave after the per-env
-// barrier - template slots, the parked obstacle pairs, the blends of its
-// state, target and obstacles - with no pair math and no second workgroup
-// barrier; a blend that leaves the fresh value's bits (a non-finite old
-// value) re-observes the wave's finished envs from the blended values
-// (reobs_block). A3/O8 at LPR 8 (configs[1]); MARLNAV_SPLIT_SPEC 0 (A/B
-// builds): the workgroup-wide fused pass (reinit_reobs_native) after a
-// barrier. (Computing each wave's own items at stage time instead put ~220
-// VALU on every wave's chain: 1024x3x8 unchanged, LPR 4 +0.4 us; drawing the
-// obstacles in the items too made waves 1..3 outlast the per-env phase.)
-template <int A, int O, int LPR>
-constexpr bool kSplitSpec = SplitPlan<A, O, LPR>::SPEC;
 template <int A, int O, int LPR>
 constexpr bool kSplitTgtInOb = !kSplitTgtInAg<A, O, LPR> && O % LPR != 0;
 
@@ -784,14 +749,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
     // (the fused native re-init of few-obstacle shapes only: at A16/O32 the
     // draws cost the stage ~1 us, more than they save in the tail)
     constexpr bool kPre = kSplitSpread<A, O> && O <= 8;
-    constexpr bool kSpec = kSplitSpec<A, O, LPR> && !NOISY && !OBS_ONLY;
-    bool spec_on = false;
-    if constexpr (kSpec) {
-        KArgsK *kl = kargs_late<kHotKargsOff>();
-        // (every wave of the workgroup live: waves 1..3 compute the items)
-        spec_on = kl->a.b.formation && kl->a.b.formation_obs && !kl->a.b.fresh_states &&
-                  live == kWavesPerBlock;
-    }
     if constexpr (kPre && !NOISY && !OBS_ONLY) {
         // native re-init: this wave's envs' fresh obstacles (Philox draws of
         // seed, step and env id), drawn while the staging loads are in
@@ -1330,55 +1287,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
                 c_tar = __popcll(__ballot(ta_l));
                 STAMPX(1);
                 if (MARLNAV_SPLIT_PRIO) __builtin_amdgcn_s_setprio(0);
-            } else if (kSpec && spec_on) {
-                if constexpr (kSpec) {
-                    // ---- kSplitSpec: waves 1..3, under wave 0's per-env
-                    // phase: item (env code c, agent ag, obstacle j) of the
-                    // workgroup's envs - the fresh obstacle (drawn into `pre`
-                    // at stage time) paired with the formation agent (pair
-                    // math as native_pair_item computes it from the blended =
-                    // fresh values); wave 1 parks the formation and its
-                    // template
-                    KArgsK *kl = kargs_late<kHotKargsOff>();
-                    const float *form = kl->a.b.formation;
-                    float *sfo = lds + kWavesPerBlock * SP::FLOATS + SP::SFORM;
-                    float2 *stp = reinterpret_cast<float2 *>(lds + kWavesPerBlock * SP::FLOATS + SP::STPL);
-                    float2 *spr = reinterpret_cast<float2 *>(lds + kWavesPerBlock * SP::FLOATS + SP::SPAIR);
-                    if (wib == 1) {
-                        if ((int)lane < 5 * A + 2) sfo[lane] = form[lane];
-                        if ((int)lane < A * A)
-                            stp[lane] = reinterpret_cast<const float2 *>(kl->a.b.formation_obs)[lane];
-                    }
-                    constexpr int NI = SP::EW * A * O;
-                    const int it = (wib - 1) * 64 + (int)lane;
-                    if (it < NI) {
-                        const int c = it / (A * O), rem = it - c * (A * O);
-                        const int ag = rem / O, j = rem - ag * O;
-                        float f[4];
-#pragma unroll
-                        for (int k2 = 0; k2 < 4; ++k2) {  // (uniform loads, selected per lane)
-                            float v = form[k2];
-#pragma unroll
-                            for (int m = 1; m < A; ++m) v = ag == m ? form[5 * m + k2] : v;
-                            f[k2] = v;
-                        }
-                        const float v[2] = {pre[(2 * j) * SP::EW + c], pre[(2 * j + 1) * SP::EW + c]};
-                        const bool cok = coord_ok(f[0]) && coord_ok(f[1]) && coord_ok(v[0]) &&
-                                         coord_ok(v[1]);
-                        bool unused = true;
-                        float d, ang;
-                        if (__ballot(!cok) == 0ull) {
-                            d = pair_dist<true>(f[0], f[1], v[0], v[1], unused);
-                            ang = pair_angle<true>(f[0], f[1], v[0], v[1], f[2], f[3], d,
-                                                   pr.cap_distance, unused);
-                        } else {
-                            d = pair_dist<false>(f[0], f[1], v[0], v[1], unused);
-                            ang = pair_angle<false>(f[0], f[1], v[0], v[1], f[2], f[3], d,
-                                                    pr.cap_distance, unused);
-                        }
-                        spr[it] = make_float2(ang, d);
-                    }
-                }
             }
             __syncthreads();
             STAMPX(2);
@@ -1393,101 +1301,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock, 4)
             // and re-observed by its own wave before the per-env barrier)
             const bool own_done = kSplitOwn<A, O, LPR, OWN> && tpl_on;
             if ((MARLNAV_AB & (1 << 19)) && list.total()) tail_wg = true;
-            const int nfin = ((MARLNAV_AB & 1) || own_done) ? 0 : list.total();  // (AB 1: timing only)
-            if (kSpec && spec_on && nfin) {
-                if constexpr (kSpec) {
-                    // ---- kSplitSpec: this wave's finished envs, on the wave
-                    // (no barrier: each wave writes and stores its own tile)
-                    bool efin = false;
-                    for (int f = 0; f < nfin; ++f) efin |= list[f] == wib * EPW + el;
-                    efin = efin && row_on;
-                    if (__ballot(efin)) {
-                        KArgsK *kl = kargs_late<kHotKargsOff>();
-                        const float *sfo = lds + kWavesPerBlock * SP::FLOATS + SP::SFORM;
-                        const float2 *stp = reinterpret_cast<const float2 *>(
-                            lds + kWavesPerBlock * SP::FLOATS + SP::STPL);
-                        const float2 *spr = reinterpret_cast<const float2 *>(
-                            lds + kWavesPerBlock * SP::FLOATS + SP::SPAIR);
-                        const int c = wib * EPW + el;  // this lane's env code
-                        const int64_t e = e0 + el;
-                        float *srow = st + 5 * rowc;
-                        float *tgl = wl + SP::TG + 2 * el;
-                        float *obl = wl + SP::OB + 2 * O * el;
-                        // every read first (old values, the parked fresh
-                        // values and pairs), then the blends
-                        // (environment.py:86-90) and every write
-                        static_assert(SP::NOB == 1 && SP::NAG == 1, "one obstacle / template slot per lane");
-                        const int jc = (O % LPR == 0 || q < O) ? q : 0;
-                        float so[5], sf[5];
-#pragma unroll
-                        for (int k2 = 0; k2 < 5; ++k2) {
-                            so[k2] = srow[k2];
-                            sf[k2] = sfo[5 * a + k2];
-                        }
-                        const float ob0 = obl[2 * jc], ob1 = obl[2 * jc + 1];
-                        const float fo0 = pre[(2 * jc) * SP::EW + c], fo1 = pre[(2 * jc + 1) * SP::EW + c];
-                        const float to0 = tgl[0], to1 = tgl[1];
-                        const float ft0 = sfo[5 * A], ft1 = sfo[5 * A + 1];
-                        const float2 sp = spr[(c * A + a) * O + jc];
-                        const bool valid = q < A - 1, tgt = q == LPR - 1;
-                        const float2 tv = stp[a * A + (valid ? q + 1 : 0)];
-                        float sb[5];
-                        bool uncl = false;
-#pragma unroll
-                        for (int k2 = 0; k2 < 5; ++k2) {
-                            sb[k2] = blend_in(so[k2], sf[k2]);
-                            if (k2 < 4) uncl |= __float_as_uint(sb[k2]) != __float_as_uint(sf[k2]);
-                        }
-                        const float tb0 = blend_in(to0, ft0), tb1 = blend_in(to1, ft1);
-                        const float ob0b = blend_in(ob0, fo0), ob1b = blend_in(ob1, fo1);
-                        uncl |= __float_as_uint(tb0) != __float_as_uint(ft0) ||
-                                __float_as_uint(tb1) != __float_as_uint(ft1) ||
-                                __float_as_uint(ob0b) != __float_as_uint(fo0) ||
-                                __float_as_uint(ob1b) != __float_as_uint(fo1);
-                        wave_sync();  // every lane has read the old values
-                        if (efin && q == 0) {
-#pragma unroll
-                            for (int k2 = 0; k2 < 5; ++k2) srow[k2] = sb[k2];
-                        }
-                        if (efin && a == 0 && (O % LPR == 0 || q < O)) {
-                            obl[2 * q] = ob0b;
-                            obl[2 * q + 1] = ob1b;
-                            out_el(kl->a.b.obstacles, e * O * 2 + 2 * q, ob0b);
-                            out_el(kl->a.b.obstacles, e * O * 2 + 2 * q + 1, ob1b);
-                            if (q == 0) {
-                                tgl[0] = tb0;
-                                tgl[1] = tb1;
-                                out_el(kl->a.b.target, 2 * e, tb0);
-                                out_el(kl->a.b.target, 2 * e + 1, tb1);
-                            }
-                        }
-                        wave_sync();
-                        if (__ballot(efin && uncl) == 0ull) {
-                            if (efin) {  // the fresh rows: obstacle pair and template slot
-                                if (O % LPR == 0 || q < O) {
-                                    orow[2 + q] = sp.x;
-                                    orow[2 + O + q] = sp.y;
-                                }
-                                if (valid || tgt) {
-                                    const int sa = valid ? 2 + 2 * O + q : 0;
-                                    const int sd = valid ? 2 + 2 * O + (A - 1) + q : 1;
-                                    orow[sa] = tv.y < pr.cap_distance ? 0.0f : tv.x;  // :172-177
-                                    orow[sd] = tv.y;
-                                }
-                            }
-                        } else {
-                            // a blend left the fresh bits: every pair of the
-                            // wave's finished envs from the blended values
-                            const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS,
-                                            SP::DP> ev{lds, blk0 * EPW};
-                            for (int cl = 0; cl < EPW; ++cl)
-                                if (__ballot(efin && el == cl))
-                                    reobs_block<A, O>(ev, OneEnv{wib * EPW + cl}, 1, pr.cap_distance,
-                                                      (int)lane, 64);
-                        }
-                    }
-                }
-            } else if (nfin) {
+            if (const int nfin = ((MARLNAV_AB & 1) || own_done) ? 0 : list.total()) {  // (AB 1: timing only)
                 KArgsK *kl = kargs_late<kHotKargsOff>();
                 const SplitEnvs<A, O, EPW, SP::FLOATS, SP::ST, SP::OB, SP::TG, SP::OBS, SP::DP> ev{
                     lds, blk0 * EPW};

@@ -164,7 +164,10 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // instantiation: every lane moves all A agents of its env, no move barrier;
 // bit-exact, +0.4 us at 16384x3x3); at 16437ed: MARLNAV_BLOCK_PIPE (two
 // env blocks per workgroup, software-pipelined: bit-exact, 65536x3x3 6.44 ->
-// 9.45 us, profiles/r06_ab_pipe.txt).
+// 9.45 us, profiles/r06_ab_pipe.txt); at eb3feb8: MARLNAV_SPLIT_SPEC (split
+// kernel A3/O8: a finished env's fresh rows from obstacle pairs computed
+// speculatively for every env; bit-exact, 1024x3x8 4.85 -> 4.85-4.94 us,
+// profiles/r06_ab_split_spec.txt).
 // Round 5 (DESIGN.md §5 "Round 5"; code in git history at deae14b):
 // MARLNAV_BLOCK_ENV_ROT / MARLNAV_SPLIT_ENV_ROT (the per-env phase on wave
 // block % A / workgroup % 4: no gain, and the general re-init thread index
@@ -190,13 +193,6 @@ typedef __attribute__((address_space(1))) unsigned long long stamp_t;
 // The same in the pair-split kernel's split_pairs (A16/O32, A3/O8 small
 // grids): 4096x16x32 11.19 -> 11.33 us, 1024x3x8 and 2048x16x32 unchanged
 // (profiles/r06_ab_packed_split.txt): off (A/B builds: 1)
-// Split kernel, few-obstacle spread shapes (A3/O8): a finished env's fresh
-// rows from obstacle pairs computed speculatively at stage time, written by
-// its own wave (1), or the workgroup-wide fused re-init pass after a barrier
-// (0; A/B builds). kernel_split.h kSplitSpec.
-#ifndef MARLNAV_SPLIT_SPEC
-#define MARLNAV_SPLIT_SPEC 1
-#endif
 #ifndef MARLNAV_PACKED_SPLIT
 #define MARLNAV_PACKED_SPLIT 0
 #endif

@@ -244,11 +244,12 @@ def test_native_trajectory_bit_exact_vs_oracle(pkg, P, A, O, steps, ep):
                                             (1000 + 3, 3, 8, True)])
 def test_native_a3o8_finished_env_paths_bit_exact_vs_oracle(pkg, P, A, O, template):
     """The split kernel's A3/O8 finished envs (native re-init, two-step
-    episodes: many finish every step) through both of its paths: with the
-    formation template (kSplitSpec: the fresh rows from obstacle pairs
-    computed at stage time, written by the env's own wave) and without it (a
-    C-ABI caller that passes no formation_obs: the workgroup-wide fused pass),
-    at LPR 8 (1003 envs, a partial last tile) and LPR 4 (2053 envs)."""
+    episodes: every env finishes every other step) through the workgroup-wide
+    fused re-init pass, with the formation template passed and without it (a
+    C-ABI caller that passes no formation_obs), at LPR 8 (1003 envs, a
+    partial last tile) and LPR 4 (2053 envs). (Round 6 also ran this against
+    the speculative fresh-row variant, MARLNAV_SPLIT_SPEC at eb3feb8, which
+    took the template path.)"""
     g = torch.Generator().manual_seed(P + 17 * template)
     env = make_env(pkg, P, A, O, episode_len=2, seed=7)
     if not template:
