@@ -38,7 +38,8 @@ kernel duration of back-to-back launches measures. ``traffic``: HBM bytes per
 launch from the committed rocprofv3 PMC summary for this config (profiles/;
 not measured in this run - the source is named), or null.
 
-cpu_baseline (rank 0, every N; after the timed region): oracle/torch_ref.py - the reference's step
+cpu_baseline (rank 0 of an N=1 run, after the timed region; null at N>1 unless
+--cpu-baseline on): oracle/torch_ref.py - the reference's step
 restated with its own execution structure in eager PyTorch (pinned bit for
 bit to the reference's golden vectors, tests/test_torch_ref.py) - timed on
 the host CPU with all available cores and with one thread on a bounded
@@ -404,7 +405,8 @@ def main():
     traffic, traffic_src = load_traffic(a.pmc, f"P{P}_A{A}_O{O}")
 
     cpu = None
-    want_cpu = a.cpu_baseline in ("on", "auto")
+    # (the CPU baseline belongs to the N=1 line; --cpu-baseline on forces it)
+    want_cpu = a.cpu_baseline == "on" or (a.cpu_baseline == "auto" and world == 1)
     if rank == 0 and want_cpu:
         cpu = cpu_baseline(P, A, O, a.cpu_seconds, device)
 
@@ -440,6 +442,9 @@ def main():
                          "alg_bytes_per_launch": launch_bytes,
                          "alg_bytes_per_env_step": per_env},
             "cpu_baseline": cpu,
+            **({} if cpu is not None else
+               {"cpu_baseline_note": "off" if a.cpu_baseline == "off"
+                else "measured on rank 0 of the N=1 run only"}),
             "prewarm": {"seconds": a.prewarm, "scratch_env_steps": prewarm_steps},
             "episode_counters": counters,
             "ranks": [{"rank": r, "env_offset": off, "envs": n} for r, off, n in slices],
