@@ -22,16 +22,18 @@ clocks, which at the driver's 20-step setting was the difference between
 barrier + synchronize; K timed steps; synchronize + barrier; the max over
 ranks. value = N*P*K / max time.
 
-roofline (the step kernel): ``launch_us`` = the timed region's time per step
-(= ``ms_per_step``; one launch per step, the region's fixed synchronisation
-cost included, so ``frac`` is a lower bound that agrees with a rocprofv3
-average of the same launches); ``achieved`` = algorithmic bytes per launch
-(read 28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at A3/O3) /
-``launch_us``, against the 8 TB/s HBM peak. Beside it: ``event_launch_us``,
-HIP events on the launch stream around further, untimed passes of the same K
-steps (the timed pass itself carries no events: recording one there adds
-~13 us of GPU-side marker processing per region, scripts/diag/sync_overhead.py),
-each started behind a short device spin; the median of three. Cross-check: ``graph_replay_launch_us``, the
+roofline (the step kernel): ``launch_us`` = the step kernel's average launch
+duration by HIP events on the launch stream (``event_launch_us``): further
+passes of the same K Env.step calls right after the timed region, each behind
+a short device spin so that the events bracket the K launches back to back
+(the timed pass itself carries no events: recording one there adds ~13 us of
+GPU-side marker processing per region, scripts/diag/sync_overhead.py); the
+median of three. ``achieved`` = algorithmic bytes per launch (read
+28A+8O+13, write 20A+4A*D+11 per env-step: 336 B at A3/O3) / ``launch_us``,
+against the 8 TB/s HBM peak; it agrees with a rocprofv3 average of the same
+launches (profiles/). Beside it: ``timed_region_frac``, the same bytes over
+``ms_per_step`` (the timed region's fixed first-launch and closing
+synchronisation cost included: a lower bound). Cross-check: ``graph_replay_launch_us``, the
 same launches back to back from a hipGraph of a second Env of the same shape
 (the timed env's state and counters untouched), which is what a rocprofv3
 kernel duration of back-to-back launches measures. ``traffic``: HBM bytes per
@@ -395,13 +397,15 @@ def main():
     del kenv
     per_env = alg_bytes_per_env(A, O)
     launch_bytes = per_env * P
-    # roofline.achieved: algorithmic bytes per launch over the timed region's
-    # time per step (one launch per step; this includes the region's fixed
-    # synchronisation cost, so it is a lower bound on the kernel's own rate
-    # and agrees with a rocprofv3 average of the same launches). The event
-    # and graph-replay figures are kept beside it.
+    # roofline.achieved: algorithmic bytes per launch over the event-timed
+    # average launch duration (above, which agrees with a rocprofv3 average of
+    # the same launches); timed_region_frac: over the timed region's time per
+    # step (one launch per step, the region's fixed synchronisation cost
+    # included: a lower bound on the kernel's own rate). The graph-replay
+    # figure is kept beside them.
     step_us = dt * 1e6 / a.steps
-    achieved = launch_bytes / (step_us * 1e-6) / 1e9
+    achieved = launch_bytes / (region_us * 1e-6) / 1e9
+    timed_frac = launch_bytes / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS
     traffic, traffic_src = load_traffic(a.pmc, f"P{P}_A{A}_O{O}")
 
     cpu = None
@@ -433,8 +437,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "launch_us": step_us,
-                         "launch_us_source": "timed region (ms_per_step)",
+                         "launch_us": region_us,
+                         "launch_us_source": "HIP events on the launch stream, K back-to-back "
+                                             "Env.step launches after the timed region (median of 3)",
+                         "timed_region_frac": timed_frac,
+                         "timed_region_launch_us": step_us,
                          "event_launch_us": region_us,
                          "event_launch_us_passes": regions,
                          "graph_replay_launch_us": kern_us,
