@@ -74,6 +74,13 @@ __device__ __forceinline__ void out_st4(float *p, float4 v)
 // 8 -> 2 MB: 16384x3x3 5.33 -> 5.17 us, 32768x3x3 6.23 -> 5.91, 512x16x32
 // 8.31 -> 8.06, 1024x16x32 8.85 -> 8.38; 8192x3x3 (1.8 MB) stays at 5.05
 // below it (5.11 written through); 0 MB would take 2x3x3 3.01 -> 3.11.
+// Round 6, final kernels, one box, stream launches / graph replay
+// (scripts/diag/launch_modes.py, profiles/r06_ab_wt_min.txt): written through
+// at every size against the 2 MB threshold: 8192x3x3 (1.8 MB) 5.08 -> 4.88 /
+// 4.57 -> 4.34 us, 4096x3x3 4.92 -> 4.83 / 4.41 -> 4.30, 2048x3x8 5.45 ->
+// 5.31 / 5.13 -> 5.02, 1024x3x8 (configs[1]) 4.96 -> 4.90 / 4.65 -> 4.59,
+// 512x3x8 4.85 -> 4.80 / 4.59 -> 4.54, 256x3x3 4.47 -> 4.48 / 4.13 -> 4.05,
+// but 2x3x3 (configs[0]) 2.85 -> 3.24 / 2.75 -> 2.91: the threshold is 64 KB.
 // marlnav_step / marlnav_observe set kWriteThroughFlag in
 // MarlnavParams.flags; `wt` in the kernels is that bit.
 #ifndef MARLNAV_CPOL
@@ -82,10 +89,10 @@ __device__ __forceinline__ void out_st4(float *p, float4 v)
 constexpr int kCpolOut = MARLNAV_CPOL < 0 ? 0 : MARLNAV_CPOL;
 constexpr bool kWtOut = MARLNAV_CPOL >= 0;
 constexpr uint32_t kWriteThroughFlag = 1u << 29;  // internal MarlnavParams.flags bit
-#ifndef MARLNAV_WT_MIN_MB
-#define MARLNAV_WT_MIN_MB 2
+#ifndef MARLNAV_WT_MIN_KB
+#define MARLNAV_WT_MIN_KB 64
 #endif
-constexpr int64_t kWriteThroughMinBytes = (int64_t)MARLNAV_WT_MIN_MB << 20;
+constexpr int64_t kWriteThroughMinBytes = (int64_t)MARLNAV_WT_MIN_KB << 10;
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v2i_t __attribute__((ext_vector_type(2)));
 
