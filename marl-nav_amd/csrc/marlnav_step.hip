@@ -288,7 +288,10 @@ const SplitVariant kSplitVariants[] = {
     MARLNAV_SPLIT_VARIANT(3, 8, 8, false),
     MARLNAV_SPLIT_VARIANT(3, 3, 8, false),
 };
-constexpr int64_t kSplitTinyWaves = 256;
+#ifndef MARLNAV_SPLIT_TINY_WAVES
+#define MARLNAV_SPLIT_TINY_WAVES 256  // (A/B builds)
+#endif
+constexpr int64_t kSplitTinyWaves = MARLNAV_SPLIT_TINY_WAVES;
 // kSplitOwn (a finished env re-initialised by its own wave) for grids of at
 // most two waves per SIMD (one env per wave): same box, graph replay,
 // steady (profiles/r05_ab_tail_own2.txt, r05_ab_tail_ablate.txt): 512x16x32

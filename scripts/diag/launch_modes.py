@@ -23,6 +23,9 @@ def main():
     params = pkg.set_env_params(pkg.default_args(num_parallel=P, num_agents=A, num_obstacles=O), dev)
     params.update(rng="native", seed=20251003)
     env = pkg.Env(params)
+    fam = int(os.environ.get("MARLNAV_FORCE_FAMILY", "0"))  # (include/marlnav.h MARLNAV_FAMILY_*)
+    if fam:
+        assert env._lib.marlnav_debug_force_family(fam) == 0
     bench.prewarm(pkg.Env(params), acts, 0.3)
     for i in range(300):  # the steady mix of finished envs
         env.step(acts[i % 16])
