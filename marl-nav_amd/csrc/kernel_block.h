@@ -181,10 +181,14 @@ __device__ __forceinline__ EnvEnd env_end(F flag, float step_num_old, uint8_t te
 // long against the burst and loses at A3/O3 (graph replay, early vs after,
 // profiles/r04_ab_early_out.txt: 65536x3x8 10.54 -> 9.81 us, 131072x3x8
 // 18.10 -> 17.44, 32768x3x8 8.19 -> 8.07; 65536x3x3 6.98 -> 7.13, 16384x3x3
-// 5.18 -> 5.29, 131072x3x3 11.43 -> 11.53). MARLNAV_EARLY_OUT 0 / 1 forces it
-// (A/B builds).
-template <int A, int O>
-constexpr bool kBlockEarlyOut = MARLNAV_EARLY_OUT < 0 ? O >= 8 : MARLNAV_EARLY_OUT != 0;
+// 5.18 -> 5.29, 131072x3x3 11.43 -> 11.53). Round 6, final kernels, re-measured
+// at A3/O3 (profiles/r06_ab_revalidate.txt, four runs on three boxes, graph
+// replay and stream launches): 65536x3x3 -0.03 to -0.04 us, 131072x3x3 -0.10 to
+// -0.15, 32768x3x3 +0.01, but the draw-wave instantiation (16384x3x3, one
+// block per CU) +0.08: so every instantiation but the draw-wave one.
+// MARLNAV_EARLY_OUT 0 / 1 forces it (A/B builds).
+template <int A, int O, bool HELP>
+constexpr bool kBlockEarlyOut = MARLNAV_EARLY_OUT < 0 ? (O >= 8 || !HELP) : MARLNAV_EARLY_OUT != 0;
 
 // Phases (one block barrier after each of the first four): stage | move +
 // coordinate check | observe into LDS rows | per-env phase on wave 0 while
@@ -565,7 +569,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
             }
             STAMPX(1);  // (wave 0: the per-env outputs issued)
             const uint64_t finmask = __ballot(fin);
-            early = kBlockEarlyOut<A, O> && overlap && full && !norm && finmask == 0ull;
+            early = kBlockEarlyOut<A, O, HELP> && overlap && full && !norm && finmask == 0ull;
             if (fin)
                 list[__builtin_amdgcn_mbcnt_hi((unsigned)(finmask >> 32),
                                                __builtin_amdgcn_mbcnt_lo((unsigned)finmask, 0u))] = l;
@@ -602,7 +606,7 @@ __global__ void __launch_bounds__(64 * (A + HELP))
                           .fin;
             }
             const uint64_t fm = __ballot(fin);
-            early = kBlockEarlyOut<A, O> && full && !norm && fm == 0ull;
+            early = kBlockEarlyOut<A, O, HELP> && full && !norm && fm == 0ull;
             if (early && !(MARLNAV_AB & 2))
                 block_store2<E * A * D, E * A * 5, NT - 64>(
                     gobs, obs_rows, in_sgpr(bo.states_out + e0 * (A * 5)), st, tid - 64, wt);
